@@ -1,0 +1,90 @@
+"""The oracle, pinned against the reference's own outputs (tests/golden, made by gen_golden.py).
+
+CPU only. Checks:
+  * the oracle's dense lowering is bit-identical to the arrays the reference
+    passed to scipy.optimize.milp (lowered.npz);
+  * the oracle's HiGHS sweep reproduces the reference's HALDAResult bit-exactly
+    on every profile fixture x kv_bits x mip_gap;
+  * the exact C solver (oracle/halda_exact.c) agrees with the reference's HiGHS
+    answers on every seeded synthetic instance: same status, same (w, n) where
+    the optimum is unique, objective within 1e-12 relative.
+"""
+
+import json
+
+import numpy as np
+import pytest
+
+from oracle import milp_oracle as mo
+
+from .conftest import GOLDEN
+from .helpers import fixture_fleet, golden_lowered_keys, load_golden_lowered, synth_devices
+
+
+def test_oracle_lowering_matches_reference_arrays(llama_online_model):
+    z = np.load(GOLDEN / "lowered.npz")
+    keys = golden_lowered_keys(z)
+    assert len(keys) >= 10
+    for key, (M, seed, k) in keys.items():
+        devs = synth_devices(M, seed)
+        p = mo.lower_dense(devs, llama_online_model, k, 0.5)
+        ref = load_golden_lowered(z, key)
+        for name in ("c", "lb", "ub", "integrality", "b_ub", "A_eq"):
+            assert np.array_equal(p[name], ref[name]), (key, name)
+        assert np.array_equal(p["A_ub"], ref["A_ub"]), key
+
+
+@pytest.mark.parametrize("solver", ["highs", "exact"])
+def test_oracle_sweep_matches_reference_on_fixtures(fixtures_golden, solver):
+    for key, fx in fixtures_golden["fixtures"].items():
+        devs, model = fixture_fleet(fx["folder"])
+        best, per_k = mo.halda_solve_oracle(devs, model, mip_gap=fx["mip_gap"], kv_bits=fx["kv_bits"], solver=solver)
+        ref = fx["result"]
+        assert (best["k"], best["w"], best["n"], best["sets"]) == (ref["k"], ref["w"], ref["n"], ref["sets"]), key
+        if solver == "highs":
+            assert best["obj_value"] == ref["obj_value"], key
+        else:
+            assert best["obj_value"] == pytest.approx(ref["obj_value"], rel=1e-12, abs=1e-12), key
+        ref_k = {r["k"]: r for r in fx["per_k"]}
+        for rec in per_k:
+            assert rec["success"] == ref_k[rec["k"]]["success"], (key, rec["k"])
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8, 16, 32, 64])
+def test_exact_oracle_matches_reference_synthetic(synth_golden, llama_online_model, M):
+    G = synth_golden[M]
+    for fleet in G["fleets"]:
+        devs = synth_devices(M, fleet["seed"], fleet["devices"])
+        sets = mo.sets_of(devs)
+        for rec in fleet["per_k"]:
+            p = mo.lower_dense(devs, llama_online_model, rec["k"], 0.5, sets)
+            st, x, best, second, _ = mo.exact_solve(p)
+            if not rec["success"]:
+                assert st == 2, (M, fleet["seed"], rec["k"], st)
+                continue
+            assert st == 0
+            obj = mo.objective_value(p, x)
+            assert obj == pytest.approx(rec["obj_value"], rel=1e-12, abs=1e-12)
+            w = [int(round(v)) for v in x[:M]]
+            n = [int(round(v)) for v in x[M:2 * M]]
+            if mo.uniqueness_margin_ok(best, second):
+                assert (w, n) == (rec["w"], rec["n"]), (M, fleet["seed"], rec["k"])
+
+
+def test_exact_oracle_infeasible_bounds():
+    """k > L makes W = 0 < lb(w) = 1; the reference gets a non-success status from HiGHS."""
+    from distilp_amd.common import ModelProfileSplit
+    from distilp_amd.synth import load_model_dict
+
+    model = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+    devs = synth_devices(2, 0)
+    p = mo.lower_dense(devs, model, 81, 0.5)
+    st, *_ = mo.exact_solve(p)
+    assert st == 2
+    assert not mo.highs_solve(p).success
+
+
+def test_golden_files_are_data_only():
+    """Goldens hold inputs/outputs only (no reference source text)."""
+    for p in GOLDEN.glob("*.json"):
+        json.loads(p.read_text())
