@@ -1,0 +1,259 @@
+"""ctypes binding of libhalda (include/halda.h).
+
+The product path has exactly one engine: distilp_amd/libhalda.so on a gfx950
+GPU. If the library is missing or no MI355X is visible, every call raises
+`HaldaUnavailable` — there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, Optional
+
+import numpy as np
+
+LIB_PATH = Path(os.environ.get("HALDA_LIB", Path(__file__).resolve().parent.parent / "libhalda.so"))
+
+STATUS_OPTIMAL = 0
+STATUS_LIMIT = 1
+STATUS_INFEASIBLE = 2
+STATUS_UNSUPPORTED = -1
+STATUS_TOO_LARGE = -2
+
+_c_i32p = ctypes.POINTER(ctypes.c_int32)
+_c_i64p = ctypes.POINTER(ctypes.c_int64)
+_c_dp = ctypes.POINTER(ctypes.c_double)
+_c_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class HaldaUnavailable(RuntimeError):
+    """libhalda.so is not built or no gfx950 device is present."""
+
+
+class HaldaBatchC(ctypes.Structure):
+    _fields_ = [
+        ("n_inst", ctypes.c_int32),
+        ("max_cols", ctypes.c_int32),
+        ("max_R1", ctypes.c_int32),
+        ("max_tab", ctypes.c_int32),
+        ("max_tab_kc", ctypes.c_int32),
+        ("n_cols", ctypes.c_void_p),
+        ("n_rows", ctypes.c_void_p),
+        ("csr_off", ctypes.c_void_p),
+        ("col_off", ctypes.c_void_p),
+        ("row_off", ctypes.c_void_p),
+        ("row_ptr", ctypes.c_void_p),
+        ("col_idx", ctypes.c_void_p),
+        ("val", ctypes.c_void_p),
+        ("c", ctypes.c_void_p),
+        ("col_lb", ctypes.c_void_p),
+        ("col_ub", ctypes.c_void_p),
+        ("row_lb", ctypes.c_void_p),
+        ("row_ub", ctypes.c_void_p),
+        ("integrality", ctypes.c_void_p),
+        ("mip_rel_gap", ctypes.c_double),
+        ("mip_abs_gap", ctypes.c_double),
+        ("time_limit", ctypes.c_double),
+        ("x0", ctypes.c_void_p),
+        ("y0", ctypes.c_void_p),
+    ]
+
+
+class HaldaResultC(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_void_p),
+        ("x", ctypes.c_void_p),
+        ("obj_lin", ctypes.c_void_p),
+        ("dual_bound", ctypes.c_void_p),
+        ("gap", ctypes.c_void_p),
+        ("nodes", ctypes.c_void_p),
+    ]
+
+
+EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
+           "halda_lds_bytes", "halda_last_error", "halda_free")
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: Path | str | None = None):
+    """dlopen libhalda and declare the prototypes. Raises HaldaUnavailable if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = Path(path) if path is not None else LIB_PATH
+        if not p.exists():
+            raise HaldaUnavailable(f"{p} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                                   "or `make -C distilp_amd/csrc`")
+        lib = ctypes.CDLL(str(p))
+        lib.halda_version.restype = ctypes.c_int
+        lib.halda_init.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        lib.halda_init.restype = ctypes.c_int
+        lib.halda_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC), ctypes.POINTER(HaldaResultC)]
+        lib.halda_solve_batch.restype = ctypes.c_int
+        lib.halda_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC),
+                                                 ctypes.POINTER(HaldaResultC), ctypes.c_void_p]
+        lib.halda_solve_batch_device.restype = ctypes.c_int
+        lib.halda_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        lib.halda_last_kernel_ms.restype = ctypes.c_int
+        lib.halda_lds_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.halda_lds_bytes.restype = ctypes.c_int64
+        lib.halda_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        lib.halda_last_error.restype = ctypes.c_int
+        lib.halda_free.argtypes = [ctypes.c_void_p]
+        lib.halda_free.restype = None
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def last_error(lib) -> str:
+    buf = ctypes.create_string_buffer(1024)
+    lib.halda_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+@dataclass
+class HostBatch:
+    """A batch of lowered instances in host memory (NumPy, C-contiguous)."""
+
+    n_cols: np.ndarray  # int32 [n]
+    n_rows: np.ndarray  # int32 [n]
+    csr_off: np.ndarray  # int64 [n]
+    col_off: np.ndarray  # int64 [n]
+    row_off: np.ndarray  # int64 [n]
+    row_ptr: np.ndarray  # int32
+    col_idx: np.ndarray  # int32
+    val: np.ndarray  # float64
+    c: np.ndarray
+    col_lb: np.ndarray
+    col_ub: np.ndarray
+    row_lb: np.ndarray
+    row_ub: np.ndarray
+    integrality: np.ndarray  # uint8
+    max_cols: int
+    max_R1: int
+    max_tab: int
+    max_tab_kc: int
+    mip_rel_gap: float = 1e-4
+
+    @property
+    def n_inst(self) -> int:
+        return int(self.n_cols.shape[0])
+
+    @property
+    def total_cols(self) -> int:
+        return int(self.c.shape[0])
+
+    def nbytes(self) -> int:
+        return sum(getattr(self, f).nbytes for f in ("n_cols", "n_rows", "csr_off", "col_off", "row_off", "row_ptr",
+                                                     "col_idx", "val", "c", "col_lb", "col_ub", "row_lb", "row_ub",
+                                                     "integrality"))
+
+
+@dataclass
+class BatchResult:
+    status: np.ndarray
+    x: np.ndarray
+    obj_lin: np.ndarray
+    dual_bound: np.ndarray
+    gap: np.ndarray
+    nodes: np.ndarray
+
+
+def _ptr(a: np.ndarray) -> int:
+    return int(a.ctypes.data)
+
+
+class HaldaContext:
+    """One libhalda context bound to one GPU (halda_init / halda_free)."""
+
+    def __init__(self, device: int = 0, lib=None):
+        self.lib = lib or load_library()
+        ctx = ctypes.c_void_p()
+        rc = self.lib.halda_init(int(device), ctypes.byref(ctx))
+        if rc != 0:
+            raise HaldaUnavailable(f"halda_init({device}) failed ({rc}): {last_error(self.lib)}")
+        self.ctx = ctx
+        self.device = device
+        self._lock = threading.Lock()
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.halda_free(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _batch_struct(self, b: HostBatch) -> HaldaBatchC:
+        s = HaldaBatchC()
+        s.n_inst = b.n_inst
+        s.max_cols, s.max_R1, s.max_tab, s.max_tab_kc = b.max_cols, b.max_R1, b.max_tab, b.max_tab_kc
+        for f in ("n_cols", "n_rows", "csr_off", "col_off", "row_off", "row_ptr", "col_idx", "val", "c", "col_lb",
+                  "col_ub", "row_lb", "row_ub", "integrality"):
+            setattr(s, f, _ptr(getattr(b, f)))
+        s.mip_rel_gap = b.mip_rel_gap
+        s.mip_abs_gap = 1e-6
+        s.time_limit = 3600.0
+        s.x0 = s.y0 = None
+        return s
+
+    def solve(self, b: HostBatch) -> BatchResult:
+        """halda_solve_batch on host arrays (synchronous)."""
+        n = b.n_inst
+        out = BatchResult(status=np.empty(n, np.int32), x=np.zeros(b.total_cols), obj_lin=np.empty(n),
+                          dual_bound=np.empty(n), gap=np.empty(n), nodes=np.empty(n, np.int64))
+        r = HaldaResultC(_ptr(out.status), _ptr(out.x), _ptr(out.obj_lin), _ptr(out.dual_bound), _ptr(out.gap),
+                         _ptr(out.nodes))
+        s = self._batch_struct(b)
+        with self._lock:
+            rc = self.lib.halda_solve_batch(self.ctx, ctypes.byref(s), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError(f"halda_solve_batch failed ({rc}): {last_error(self.lib)}")
+        return out
+
+    def solve_device(self, dev_ptrs: Dict[str, int], b: HostBatch, out_ptrs: Dict[str, int],
+                     stream: Optional[int] = None) -> None:
+        """halda_solve_batch_device: arrays already resident in HBM (e.g. torch tensors)."""
+        s = HaldaBatchC()
+        s.n_inst = b.n_inst
+        s.max_cols, s.max_R1, s.max_tab, s.max_tab_kc = b.max_cols, b.max_R1, b.max_tab, b.max_tab_kc
+        for f, p in dev_ptrs.items():
+            setattr(s, f, int(p))
+        s.mip_rel_gap = b.mip_rel_gap
+        s.time_limit = 3600.0
+        r = HaldaResultC(**{k: int(v) for k, v in out_ptrs.items()})
+        rc = self.lib.halda_solve_batch_device(self.ctx, ctypes.byref(s), ctypes.byref(r),
+                                               ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise RuntimeError(f"halda_solve_batch_device failed ({rc}): {last_error(self.lib)}")
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_double()
+        rc = self.lib.halda_last_kernel_ms(self.ctx, ctypes.byref(ms))
+        if rc != 0:
+            raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
+        return ms.value
+
+
+_contexts: Dict[int, HaldaContext] = {}
+_ctx_lock = threading.Lock()
+
+
+def get_context(device: int = 0) -> HaldaContext:
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = HaldaContext(device)
+            _contexts[device] = ctx
+        return ctx

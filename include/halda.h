@@ -1,0 +1,130 @@
+/*
+ * halda.h — C ABI of libhalda, the MI355X (gfx950) solver for batches of
+ * fixed-k HALDA MILPs.
+ *
+ * What it replaces. The reference (firstbatchxyz/distilp 0.1.6) solves one
+ * fixed-k MILP per (fleet, k) with
+ *     res = milp(c=c_obj, integrality=integrality, bounds=bounds,
+ *                constraints=constraints, options=options)
+ * at src/distilp/solver/halda_p_solver.py:340-346 (scipy 1.15.3 -> HiGHS
+ * 1.8.0), and reads only res.success and res.x (:347-353). One call of
+ * halda_solve_batch() stands in for a whole batch of such milp() calls: the
+ * MILP arrives in CSR form exactly as scipy would hand it to HiGHS
+ * (A = [A_ub ; A_eq], the ub rows in the reference's order then the single
+ * equality row, scipy/optimize/_milp.py:60-71), and status/x come back per
+ * instance with the same meaning as (res.success, res.x).
+ *
+ * The solve is exact (proven optimum, gap 0): libhalda validates that the CSR
+ * has the HALDA structure (columns [w|n|s1|s2|s3|t|z|C], SURVEY.md appendix
+ * A) and reduces it to a separable assignment problem that it solves by a
+ * min-plus dynamic program over sum(w) on the GPU, with a cycle-time
+ * threshold search when k > 1. A matrix without that structure is rejected
+ * with HALDA_STATUS_UNSUPPORTED, never approximated.
+ *
+ * Ownership. Every pointer in halda_batch / halda_result is owned by the
+ * caller. halda_solve_batch() takes HOST pointers, copies them to the device
+ * and keeps nothing after it returns except grow-only scratch inside ctx.
+ * halda_solve_batch_device() takes DEVICE pointers and is asynchronous on the
+ * given HIP stream. Calls on one ctx must be serialised; use one ctx per GPU.
+ * Errors: functions return 0 on success and a negative code otherwise; the
+ * message of the last failure on the calling thread is in halda_last_error().
+ */
+#ifndef HALDA_H
+#define HALDA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HALDA_ABI_VERSION 1
+
+/* per-instance status (halda_result.status) */
+#define HALDA_STATUS_OPTIMAL 0       /* res.success == True                   */
+#define HALDA_STATUS_LIMIT 1         /* reserved (time/node limit)            */
+#define HALDA_STATUS_INFEASIBLE 2    /* res.success == False (HiGHS status 2) */
+#define HALDA_STATUS_UNSUPPORTED (-1) /* CSR is not a HALDA MILP              */
+#define HALDA_STATUS_TOO_LARGE (-2)  /* exceeds the batch's shape summary     */
+
+/* return codes */
+#define HALDA_OK 0
+#define HALDA_E_ARG (-22)
+#define HALDA_E_HIP (-5)
+#define HALDA_E_NODEV (-19)
+
+typedef struct halda_batch {
+    int32_t n_inst;
+    /* Shape summary: upper bounds over the batch that size the on-chip (LDS)
+     * scratch. With M = (n_cols-1)/7, W = equality rhs and R = W - sum_i lb(w_i)
+     * (the layers left after every device's minimum), per instance:
+     *   max_cols   >= n_cols
+     *   max_R1     >= R + 1
+     *   max_tab    >= M * (R + 1)   over instances with c[C] == 0 (k == 1)
+     *   max_tab_kc >= M * (R + 1)   over instances with c[C]  > 0 (k  > 1)
+     * halda_solve_batch() (host pointers) computes them itself when all are 0.
+     * An instance exceeding them gets HALDA_STATUS_TOO_LARGE. */
+    int32_t max_cols;
+    int32_t max_R1;
+    int32_t max_tab;
+    int32_t max_tab_kc;
+    const int32_t *n_cols; /* [n_inst] N = 7M + 1 */
+    const int32_t *n_rows; /* [n_inst] ub rows + 1 eq row */
+    const int64_t *csr_off; /* [n_inst] start of the instance's row_ptr segment (n_rows + 1 entries) */
+    const int64_t *col_off; /* [n_inst] start into c / col_lb / col_ub / integrality / x */
+    const int64_t *row_off; /* [n_inst] start into row_lb / row_ub */
+    const int32_t *row_ptr; /* absolute offsets into col_idx / val; instances of one fleet may share a segment */
+    const int32_t *col_idx;
+    const double *val;
+    const double *c;
+    const double *col_lb;
+    const double *col_ub;
+    const double *row_lb; /* -inf for ub rows */
+    const double *row_ub;
+    const uint8_t *integrality;
+    double mip_rel_gap; /* accepted for API parity; the solve is exact */
+    double mip_abs_gap;
+    double time_limit;
+    const double *x0; /* optional warm start, may be NULL (unused by the exact solver) */
+    const double *y0;
+} halda_batch;
+
+typedef struct halda_result {
+    int32_t *status;     /* [n_inst] HALDA_STATUS_* */
+    double *x;           /* col_off layout, written for OPTIMAL instances */
+    double *obj_lin;     /* [n_inst] c.x */
+    double *dual_bound;  /* [n_inst] proven lower bound (== obj_lin when OPTIMAL) */
+    double *gap;         /* [n_inst] relative gap (0 when OPTIMAL) */
+    int64_t *nodes;      /* [n_inst] dynamic-programming passes evaluated */
+} halda_result;
+
+/* ABI version (HALDA_ABI_VERSION). */
+int halda_version(void);
+
+/* Bind a context to HIP device `device_ordinal` (must be gfx950). */
+int halda_init(int device_ordinal, void **ctx);
+
+/* Synchronous solve of a batch given in HOST memory (replaces a loop of milp() calls). */
+int halda_solve_batch(void *ctx, const halda_batch *in, halda_result *out);
+
+/* Asynchronous solve of a batch whose arrays are already in DEVICE memory (HBM),
+ * enqueued on `stream` (a hipStream_t; NULL = the context's stream). */
+int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out, void *stream);
+
+/* Device time of the last solve's kernel(s) in ms (valid after the stream is synchronised). */
+int halda_last_kernel_ms(void *ctx, double *ms);
+
+/* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
+int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc);
+
+/* Copy the calling thread's last error message into buf. Returns its length. */
+int halda_last_error(char *buf, size_t len);
+
+void halda_free(void *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HALDA_H */

@@ -1,0 +1,67 @@
+"""C-ABI surface of libhalda (CPU-only: loads the library, checks exports; no GPU compute)."""
+
+import ctypes
+import re
+
+import pytest
+
+from distilp_amd.solver import _libhalda as lh
+
+from .conftest import REPO
+
+HEADER = REPO / "include" / "halda.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void)\s+\**(halda_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_the_binding_exports():
+    assert declared_functions() == sorted(lh.EXPORTS)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not lh.LIB_PATH.exists():
+        pytest.fail(f"{lh.LIB_PATH} not built (run __graft_entry__.build())")
+    return lh.load_library()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    raw = ctypes.CDLL(str(lh.LIB_PATH))
+    for name in declared_functions():
+        assert hasattr(raw, name), name
+
+
+def test_version_and_lds_budget(lib):
+    assert lib.halda_version() == 1
+    # C3 shape: M = 64 (449 cols), R + 1 = 17 extra-layer states -> well under 160 KiB
+    b = lib.halda_lds_bytes(449, 17, 64 * 17, 0)
+    assert 0 < b < 64 * 1024
+    assert lib.halda_lds_bytes(449, 81, 64 * 81, 40 * 41) > b
+
+
+def test_struct_layout_matches_header():
+    # halda_batch: 5 int32 then 8-byte aligned pointers/doubles
+    assert lh.HaldaBatchC.n_cols.offset == 24
+    assert ctypes.sizeof(lh.HaldaBatchC) == 24 + 14 * 8 + 3 * 8 + 2 * 8
+    assert ctypes.sizeof(lh.HaldaResultC) == 6 * 8
+
+
+def test_init_without_gpu_fails_loudly(lib):
+    """No silent CPU fallback: without a gfx950 device halda_init returns an error code."""
+    ctx = ctypes.c_void_p()
+    rc = lib.halda_init(0, ctypes.byref(ctx))
+    if rc == 0:  # running on a GPU box
+        lib.halda_free(ctx)
+        pytest.skip("GPU present")
+    assert rc < 0
+    assert "device" in lh.last_error(lib) or "gfx950" in lh.last_error(lib)
+
+
+def test_product_path_has_no_oracle_import():
+    """The shipped package never imports the oracle (test infrastructure only)."""
+    for p in (REPO / "distilp_amd").rglob("*.py"):
+        src = p.read_text()
+        assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), p

@@ -1,0 +1,174 @@
+"""GPU parity: libhalda (HIP, gfx950) vs the reference goldens and the CPU oracle.
+
+Rule (north star): k, w, n and sets identical wherever the optimum is unique
+(uniqueness from the exact oracle's second-best margin, rel 1e-7); the objective
+within 1e-9 relative otherwise. Infeasible (fleet, k) pairs must match exactly.
+All calls go through the C ABI (distilp_amd/libhalda.so via ctypes).
+"""
+
+import numpy as np
+import pytest
+
+from distilp_amd.solver import halda_solve, halda_solve_batch
+from distilp_amd.solver._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL, get_context
+from distilp_amd.solver.batch import assemble
+from distilp_amd.solver.lower import lower_fleet
+from distilp_amd.synth import synth_fleet
+from oracle import milp_oracle as mo
+
+from .helpers import fixture_fleet, synth_devices
+
+pytestmark = pytest.mark.gpu
+
+OBJ_REL = 1e-9
+
+
+def _obj_close(a, b):
+    return abs(a - b) <= OBJ_REL * max(1.0, abs(b))
+
+
+def test_fixture_profiles_match_reference(fixtures_golden, capsys):
+    for key, fx in fixtures_golden["fixtures"].items():
+        devs, model = fixture_fleet(fx["folder"])
+        r = halda_solve(devs, model, mip_gap=fx["mip_gap"], plot=False, kv_bits=fx["kv_bits"])
+        ref = fx["result"]
+        assert (r.k, r.w, r.n, r.sets) == (ref["k"], ref["w"], ref["n"], ref["sets"]), key
+        assert _obj_close(r.obj_value, ref["obj_value"]), (key, r.obj_value, ref["obj_value"])
+        out = capsys.readouterr().out
+        assert out == fx["stdout"], key  # the "L [factors]" line, nothing else
+
+
+def _solve_fleets(fleets, model, ks):
+    lowered = [lower_fleet(devs, model, "4bit") for devs in fleets]
+    batch, refs = assemble(lowered, [ks] * len(lowered))
+    res = get_context(0).solve(batch)
+    return lowered, refs, res
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8, 16, 32, 64])
+def test_synthetic_goldens_per_instance(synth_golden, llama_online_model, M):
+    G = synth_golden[M]
+    fleets = [synth_devices(M, f["seed"], f["devices"]) for f in G["fleets"]]
+    ks = [r["k"] for r in G["fleets"][0]["per_k"]]
+    lowered, refs, res = _solve_fleets(fleets, llama_online_model, ks)
+    n_unique = 0
+    for idx, ref in enumerate(refs):
+        gold = G["fleets"][ref.fleet]["per_k"][ks.index(ref.k)]
+        st = int(res.status[idx])
+        if not gold["success"]:
+            assert st == STATUS_INFEASIBLE, (M, ref.fleet, ref.k, st)
+            continue
+        assert st == STATUS_OPTIMAL, (M, ref.fleet, ref.k, st)
+        x = res.x[ref.col_off:ref.col_off + ref.n_cols]
+        fl = lowered[ref.fleet]
+        obj = fl.objective_value(ref.c, x)
+        assert _obj_close(obj, gold["obj_value"]), (M, ref.fleet, ref.k, obj, gold["obj_value"])
+        w = [int(round(v)) for v in x[:M]]
+        n = [int(round(v)) for v in x[M:2 * M]]
+        p = mo.lower_dense(fleets[ref.fleet], llama_online_model, ref.k, 0.5)
+        _, _, b1, b2, _ = mo.exact_solve(p)
+        if mo.uniqueness_margin_ok(b1, b2):
+            n_unique += 1
+            assert (w, n) == (gold["w"], gold["n"]), (M, ref.fleet, ref.k)
+        # the GPU objective equals the proven optimum
+        assert _obj_close(float(res.obj_lin[idx]), b1)
+        assert res.dual_bound[idx] == res.obj_lin[idx] and res.gap[idx] == 0.0
+    assert n_unique > 0
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8, 16, 32, 64])
+def test_batch_api_matches_reference(synth_golden, llama_online_model, M):
+    G = synth_golden[M]
+    fleets = [synth_devices(M, f["seed"], f["devices"]) for f in G["fleets"]]
+    out = halda_solve_batch(fleets, llama_online_model, mip_gap=1e-4, kv_bits="4bit")
+    for r, f in zip(out, G["fleets"]):
+        ref = f["result"]
+        assert (r.k, r.w, r.n, r.sets) == (ref["k"], ref["w"], ref["n"], ref["sets"])
+        assert _obj_close(r.obj_value, ref["obj_value"])
+
+
+@pytest.mark.parametrize("M,seeds", [(2, range(100, 140)), (5, range(100, 130)), (12, range(100, 120)),
+                                     (24, range(100, 110)), (40, range(100, 104))])
+def test_fresh_seeds_vs_exact_oracle(llama_online_model, M, seeds):
+    """Unseen fleets (incl. M not in the goldens): GPU == exact CPU oracle."""
+    from distilp_amd.common import DeviceProfile
+
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)] for s in seeds]
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40, 3, 7]
+    lowered, refs, res = _solve_fleets(fleets, llama_online_model, ks)
+    for idx, ref in enumerate(refs):
+        p = mo.lower_dense(fleets[ref.fleet], llama_online_model, ref.k, 0.5)
+        st, xo, b1, b2, _ = mo.exact_solve(p)
+        gst = int(res.status[idx])
+        if st == 2:
+            assert gst == STATUS_INFEASIBLE
+            continue
+        assert gst == STATUS_OPTIMAL
+        x = res.x[ref.col_off:ref.col_off + ref.n_cols]
+        assert _obj_close(float(res.obj_lin[idx]), b1), (M, ref.fleet, ref.k)
+        assert _obj_close(float(np.dot(p["c"], x)), b1)
+        if mo.uniqueness_margin_ok(b1, b2):
+            assert np.array_equal(x[:2 * M], xo[:2 * M]), (M, ref.fleet, ref.k)
+
+
+def test_solution_is_feasible_and_deterministic(llama_online_model):
+    """Full-size property check (config C3 shape): feasibility of x in the MILP, Sum w = W, determinism."""
+    from distilp_amd.common import DeviceProfile
+
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, 64)] for s in range(500, 756)]
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    lowered, refs, res = _solve_fleets(fleets, llama_online_model, ks)
+    _, _, res2 = _solve_fleets(fleets, llama_online_model, ks)
+    assert np.array_equal(res.status, res2.status) and np.array_equal(res.x, res2.x)
+    for idx, ref in enumerate(refs):
+        fl = lowered[ref.fleet]
+        if ref.k > 1:
+            assert res.status[idx] == STATUS_INFEASIBLE  # M = 64 > W
+            continue
+        assert res.status[idx] == STATUS_OPTIMAL
+        x = res.x[ref.col_off:ref.col_off + ref.n_cols]
+        A = fl.dense()
+        act = A @ x
+        c, lb, ub, row_lb, row_ub, integ, W = fl.instance(ref.k)
+        slack_tol = 1e-6 * np.maximum(1.0, np.abs(row_ub))
+        assert np.all(act <= row_ub + slack_tol)
+        assert np.all(act >= row_lb - slack_tol)
+        assert np.all(x >= lb) and np.all(x <= ub)
+        assert int(x[:fl.M].sum()) == W
+        xi = x[integ.astype(bool)]
+        assert np.array_equal(xi, np.round(xi))
+
+
+def test_edge_k_candidates(llama_online_model, capsys):
+    devs = synth_devices(2, 0)
+    # k > L: W = 0 < lb(w) -> infeasible; non-divisor k: W = L // k; duplicates removed
+    r = halda_solve(devs, llama_online_model, k_candidates=[3, 3, 81, 7], plot=False, kv_bits="4bit")
+    best, per_k = mo.halda_solve_oracle(devs, llama_online_model, k_candidates=[3, 81, 7], kv_bits="4bit",
+                                        solver="highs")
+    assert (r.k, r.w, r.n) == (best["k"], best["w"], best["n"])
+    assert capsys.readouterr().out == ""  # explicit k list: no factor print
+    with pytest.raises(RuntimeError, match="No feasible MILP found for any k this round."):
+        halda_solve(devs, llama_online_model, k_candidates=[81, 100], plot=False)
+    with pytest.raises(ZeroDivisionError):
+        halda_solve(devs, llama_online_model, k_candidates=[0, 1], plot=False)
+    with pytest.raises(ValueError, match="Unsupported kv_bits"):
+        halda_solve(devs, llama_online_model, kv_bits="2bit", plot=False)
+
+
+def test_unsupported_structure_is_rejected(llama_online_model):
+    devs = synth_devices(3, 1)
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    batch, refs = assemble([fl], [[1, 2]])
+    batch.val = batch.val.copy()
+    batch.val[0] = 0.5  # link row n - w <= 0 becomes n - 0.5 w <= 0: not a HALDA row
+    res = get_context(0).solve(batch)
+    assert list(res.status) == [-1, -1]
+
+
+def test_debug_output_format(llama_online_model, capsys):
+    devs, model = fixture_fleet("llama_3_70b/online")
+    halda_solve(devs, model, plot=False, debug=True, kv_bits="4bit", k_candidates=[1, 2, 80])
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "Objectives by k"
+    assert out[1] == "k: 1" and out[2].startswith("  k=1     obj=")
+    assert out[-1] == "  k=80    obj=infeasible"
