@@ -4,24 +4,31 @@
 // reference at src/distilp/solver/halda_p_solver.py:340-346; the C ABI is in
 // include/halda.h, the design (and why the DP is exact) in DESIGN.md.
 //
-// One 256-thread workgroup (4 wave64s) solves one instance, entirely on chip:
-//   1. validate + decode the CSR MILP into per-device records in LDS (every
-//      thread owns rows / devices; the CSR, bounds and costs are read once,
-//      coalesced, from HBM);
-//   2. table phase: for every device i and every extra-layer count
-//      e = w_i - lb(w_i) in [0, R], R = W - sum_i lb(w_i), find the best GPU
-//      split n (the cost is convex piecewise-linear in n, so only the interval
-//      ends and the slack kinks are evaluated) -> G[i][e] (cost), H[i][e]
-//      (least cycle time, only when k > 1);
-//   3. wave 0 runs a min-plus DP over sum(e) (state width R + 1, which is the
-//      slack of the problem, 17 at M=64/W=80), and for k > 1 a pruned
-//      ascending scan over cycle-time thresholds T (min (k-1)T + S(T));
-//   4. backtrack, then all threads rebuild x (w, n, slacks, stalls z, cycle C).
-// All floating-point arithmetic keeps the reference's operation order
-// (compiled with -ffp-contract=off).
+// A batch is solved by two launches on one stream:
+//   screen   one wave per instance: validates the equality row and the
+//            column bounds, settles bound-infeasible instances (sum lb(w) > W,
+//            every k with M > L/k) and non-HALDA inputs right there, and
+//            flags the rest (class 1: k = 1, class 2: k > 1);
+//   solve    persistent 64-thread workgroups (= one wave each, no barriers),
+//            each owning instances blockIdx + j * gridDim (a ballot over the
+//            screen verdicts skips the settled ones), with its own LDS slice:
+//            rows    decode the CSR rows (lane-strided) into per-device
+//                    records in LDS, validating the HALDA pattern;
+//            tables  lane = device: for every extra-layer count e in [0, R]
+//                    (w = lb(w) + e, R = W - sum lb(w)) the best GPU split n
+//                    (cost convex piecewise-linear in n -> only interval ends
+//                    and slack kinks are evaluated): G[e][i] cost, H[e][i]
+//                    least cycle time (k > 1 only);
+//            DP      min-plus DP over sum(e) as a balanced tree of pairwise
+//                    convolutions (lanes = (node, state) tasks), argmin splits
+//                    kept for a parallel top-down backtrack; k > 1 adds a
+//                    pruned ascending scan over cycle-time thresholds T;
+//            output  lane = device rebuilds x for its chosen w.
+// Floating point keeps the reference's operation order (-ffp-contract=off).
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -33,67 +40,53 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
-constexpr int kRows = 4;             // capacity rows per device (link, RAM/Metal cap, <= 2 VRAM)
-constexpr int kMaxRowNnz = 8;        // widest HALDA row (cycle rows: 6 device cols + z + C)
-constexpr double kSlackEps = 1e-9;   // a capacity row counts as met within 1e-9 layers (oracle: same)
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kRows = 4;            // capacity rows per device (link, RAM/Metal cap, <= 2 VRAM)
+constexpr int kMaxRowNnz = 8;       // widest HALDA row (cycle rows: 6 device cols + z + C)
+constexpr double kSlackEps = 1e-9;  // a capacity row counts as met within 1e-9 layers (oracle: same)
 constexpr double kInf = __builtin_huge_val();
 
-// per-device double fields (SoA, index f * Mmax + i)
-enum { DD_CW, DD_CN, DD_CS0, DD_CS1, DD_CS2, DD_CS3, DD_R1W, DD_R2W, DD_RHS1, DD_RHS2, DD_G, DD_H, kDevD };
-// per-device int fields
-enum {
-    DI_WLO, DI_WHI, DI_NLO, DI_NHI, DI_SLO0, DI_SLO1, DI_SLO2, DI_SLO3,
-    DI_SHI0, DI_SHI1, DI_SHI2, DI_SHI3, DI_NROW, DI_HAVE1, DI_HAVE2, DI_WSOL, kDevI
-};
-// block scalars (ints)
-enum { SC_FLAGS, SC_SUMWLO, SC_NODES, SC_STATUS, kScI = 8 };
-// flag bits
-enum { F_UNSUPPORTED = 1, F_INFEASIBLE = 2, F_TOO_LARGE = 4 };
+enum { CLS_DONE = 0, CLS_K1 = 1, CLS_KC = 2 };  // screen verdicts
 
-struct Layout {
-    int64_t dd, di, rows, tab, choice, dp, red, sci, total;
+// ---------------------------------------------------------------- LDS slice
+// One solve wave = one 64-thread workgroup with its own LDS slice (bytes):
+//   rows   per device kRows x int2 {pack(kind + 1, u + 1, v + 1), K}
+//   cyc    per device {r1w, r2w, rhs1, rhs2} (cycle-row w coefficients and rhs)
+//   cnt    per device row counter | have1 << 8 | have2 << 16
+//   st0/1  per device ints (DP backtracking states, ping-pong)
+//   G      [i][e] table, row stride RS (odd), leaves of the DP tree; k = 1 reduces in place
+//   H      [i][e] least cycle time (k > 1 only)
+//   work   DP tree levels when the leaves must survive (k > 1 threshold scan)
+//   split  DP tree argmin (uint8 e of the left subtree), ~M * (R + 1) bytes
+struct Slice {
+    int64_t rows, cyc, cnt, st0, st1, G, H, work, split, total;
 };
 
 __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
-__host__ __device__ inline Layout make_layout(int mmax, int r1max, int tab, int tab_kc) {
-    Layout L;
+// tab / tab_kc count M * RS doubles (RS = R + 1 rounded up to odd)
+__host__ __device__ inline Slice make_slice(int mmax, int r1max, int tab, int tab_kc) {
+    Slice s;
     int64_t o = 0;
-    L.dd = o;     o = align16(o + int64_t(mmax) * kDevD * 8);
-    L.di = o;     o = align16(o + int64_t(mmax) * kDevI * 4);
-    L.rows = o;   o = align16(o + int64_t(mmax) * kRows * 16);
-    int64_t tb = int64_t(tab) * 8 > int64_t(tab_kc) * 16 ? int64_t(tab) * 8 : int64_t(tab_kc) * 16;
-    L.tab = o;    o = align16(o + tb);
-    L.choice = o; o = align16(o + (tab > tab_kc ? tab : tab_kc));
-    L.dp = o;     o = align16(o + 2 * int64_t(r1max) * 8);
-    L.red = o;    o = align16(o + 8 * kWaves * 2);
-    L.sci = o;    o = align16(o + 4 * kScI);
-    L.total = o;
-    return L;
+    const int64_t tmax = tab > tab_kc ? tab : tab_kc;
+    s.rows = o;  o = align16(o + int64_t(mmax) * kRows * 8);
+    s.cyc = o;   o = align16(o + int64_t(mmax) * 4 * 8);
+    s.cnt = o;   o = align16(o + int64_t(mmax) * 4);
+    s.st0 = o;   o = align16(o + int64_t(mmax) * 4);
+    s.st1 = o;   o = align16(o + int64_t(mmax) * 4);
+    s.G = o;     o = align16(o + tmax * 8);
+    s.H = o;     o = align16(o + int64_t(tab_kc) * 8);
+    s.work = o;  o = align16(o + (tab_kc > 0 ? (int64_t(tab_kc) / 2 + 2 * int64_t(r1max) + 2) * 8 : 0));
+    s.split = o; o = align16(o + (int64_t(mmax) + 12) * r1max);
+    s.total = o;
+    return s;
 }
-
-struct Lds {
-    double *dd;
-    int *di;
-    int *rows;
-    double *G, *H;
-    uint8_t *choice;
-    double *D0, *D1;
-    double *red;
-    int *sc;
-    int mmax;
-    __device__ double &d(int f, int i) const { return dd[f * mmax + i]; }
-    __device__ int &n(int f, int i) const { return di[f * mmax + i]; }
-    __device__ int *row(int i, int q) const { return rows + (i * kRows + q) * 4; }
-};
 
 __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-
 __device__ inline double wave_min(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
@@ -102,436 +95,669 @@ __device__ inline double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
 }
-
-// Least slacks (s1, s2, s3, t) for integer (w, n); false when a row cannot be met.
-// Row (kind, u, v, K): slack rows need s_kind >= u*w + v*n + K with
-// K = ceil(-rhs/beta - eps); pure (w, n) rows need u*w + v*n <= K.
-__device__ inline bool least_slacks(const Lds &L, int i, int w, int n, int s[4]) {
-    s[0] = L.n(DI_SLO0, i); s[1] = L.n(DI_SLO1, i); s[2] = L.n(DI_SLO2, i); s[3] = L.n(DI_SLO3, i);
-    const int nr = L.n(DI_NROW, i);
-    for (int q = 0; q < nr; ++q) {
-        const int *r = L.row(i, q);
-        const int val = r[1] * w + r[2] * n;
-        if (r[0] < 0) {
-            if (val > r[3]) return false;
-        } else {
-            const int need = val + r[3];
-            if (need > s[r[0]]) s[r[0]] = need;
-        }
-    }
-    return s[0] <= L.n(DI_SHI0, i) && s[1] <= L.n(DI_SHI1, i) && s[2] <= L.n(DI_SHI2, i) &&
-           s[3] <= L.n(DI_SHI3, i);
+__device__ inline int wave_or(int v) {
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+__device__ inline int wave_sum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
-// Objective contribution of device i (same term order as c.x in the reference).
-__device__ inline double dev_cost(const Lds &L, int i, int w, int n, const int s[4]) {
-    double g = L.d(DD_CW, i) * double(w);
-    g = g + L.d(DD_CN, i) * double(n);
-    g = g + L.d(DD_CS0, i) * double(s[0]);
-    g = g + L.d(DD_CS1, i) * double(s[1]);
-    g = g + L.d(DD_CS2, i) * double(s[2]);
-    g = g + L.d(DD_CS3, i) * double(s[3]);
+__device__ inline void write_done(const halda_result &R, int inst, int status, int64_t nodes) {
+    R.status[inst] = status;
+    R.nodes[inst] = nodes;
+    R.obj_lin[inst] = kInf;
+    R.dual_bound[inst] = status == HALDA_STATUS_INFEASIBLE ? kInf : -kInf;
+    R.gap[inst] = kInf;
+}
+
+__host__ __device__ inline int odd_stride(int r1) { return r1 | 1; }
+
+// ---------------------------------------------------------------- screen
+// One wave per instance. Settles everything decidable from the equality row and
+// the w bounds (non-HALDA shape, bound infeasibility such as M > W = L/k) and
+// flags the rest for the solve kernel (class 1: c[C] == 0, class 2: c[C] > 0).
+__global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls,
+                                                                int mmax, int r1max, int tab, int tab_kc) {
+    const int lane = threadIdx.x & 63;
+    const int inst = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (inst >= B.n_inst) return;
+    const int N = B.n_cols[inst], m = B.n_rows[inst];
+    int status = 0;  // 0 = still open
+    if (N < 1 || (N - 1) % 7 != 0 || m < 1) status = HALDA_STATUS_UNSUPPORTED;
+    const int M = (N - 1) / 7;
+    if (!status && M > mmax) status = HALDA_STATUS_TOO_LARGE;
+    if (!status) {
+        const int64_t co = B.col_off[inst], ro = B.row_off[inst];
+        const int32_t *rp = B.row_ptr + B.csr_off[inst];
+        const double Wd = B.row_ub[ro + m - 1];
+        const int eqs = rp[m - 1], eqe = rp[m];
+        if (!(B.row_lb[ro + m - 1] == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M) {
+            status = HALDA_STATUS_UNSUPPORTED;
+        } else {
+            const int W = int(Wd);
+            int bad = 0, infeas = 0, sumlo = 0;
+            for (int i = lane; i < M; i += 64) {
+                bad |= B.col_idx[eqs + i] != i || B.val[eqs + i] != 1.0;
+                const double lb = B.col_lb[co + i], ub = B.col_ub[co + i];
+                const int wlo = int(ceil(lb)), whi = int(floor(fmin(ub, Wd)));
+                infeas |= wlo > whi || lb < 0.0;
+                sumlo += wlo;
+            }
+            bad = wave_or(bad);
+            infeas = wave_or(infeas);
+            sumlo = wave_sum(sumlo);
+            if (bad) status = HALDA_STATUS_UNSUPPORTED;
+            else if (infeas || sumlo > W) status = HALDA_STATUS_INFEASIBLE;
+            else {
+                const int R1 = W - sumlo + 1;
+                const bool kc = B.c[co + 7 * M] > 0.0;
+                if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
+                else if (lane == 0) cls[inst] = kc ? CLS_KC : CLS_K1;
+            }
+        }
+    }
+    if (status && lane == 0) {
+        cls[inst] = CLS_DONE;
+        write_done(Rz, inst, status, 0);
+    }
+}
+
+// ---------------------------------------------------------------- solve
+// One device's data in registers (lane = device). Rows are regrouped per
+// slack: slack j has up to two rows (a, b) with need = u w + v n + K; pure
+// (w, n) rows (link n <= w) are the two "f" rows: u w + v n <= K.
+struct Dev {
+    double cw, cn, cs0, cs1, cs2, cs3, r1w, r2w, rhs1, rhs2;
+    int wlo, whi, nlo, nhi;
+    int slo[4], shi[4];
+    int ua[4], va[4], Ka[4], ub[4], vb[4], Kb[4];
+    int uf[2], vf[2], Kf[2];
+};
+
+constexpr int kNoRow = -(1 << 29);  // K of an absent row: never binds
+
+// Least slacks for integer (w, n); false when a row or a slack bound cannot be met.
+__device__ inline bool least_slacks(const Dev &d, int w, int n, int s[4]) {
+    bool ok = d.uf[0] * w + d.vf[0] * n <= d.Kf[0] && d.uf[1] * w + d.vf[1] * n <= d.Kf[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int a = d.ua[j] * w + d.va[j] * n + d.Ka[j];
+        const int b = d.ub[j] * w + d.vb[j] * n + d.Kb[j];
+        s[j] = max(d.slo[j], max(a, b));
+        ok = ok && s[j] <= d.shi[j];
+    }
+    return ok;
+}
+
+// Objective contribution (same term order as c.x in the reference).
+__device__ inline double dev_cost(const Dev &d, int w, int n, const int s[4]) {
+    double g = d.cw * double(w);
+    g = g + d.cn * double(n);
+    g = g + d.cs0 * double(s[0]);
+    g = g + d.cs1 * double(s[1]);
+    g = g + d.cs2 * double(s[2]);
+    g = g + d.cs3 * double(s[3]);
     return g;
 }
 
-// Cycle rows: C >= P + z, C >= Q - z with z >= 0  ->  least C = max(P, (P+Q)/2).
-__device__ inline void dev_cycle(const Lds &L, int i, int w, int n, const int s[4], double &P, double &Q) {
-    double a1 = L.d(DD_R1W, i) * double(w), a2 = L.d(DD_R2W, i) * double(w);
-    const double tail[5] = {L.d(DD_CN, i) * double(n), L.d(DD_CS0, i) * double(s[0]), L.d(DD_CS1, i) * double(s[1]),
-                            L.d(DD_CS2, i) * double(s[2]), L.d(DD_CS3, i) * double(s[3])};
-#pragma unroll
-    for (int b = 0; b < 5; ++b) {
-        a1 = a1 + tail[b];
-        a2 = a2 + tail[b];
-    }
-    P = a1 - L.d(DD_RHS1, i);
-    Q = a2 - L.d(DD_RHS2, i);
+// Cycle rows: C >= P + z, C >= Q - z, z >= 0  ->  least C = max(P, (P + Q) / 2).
+__device__ inline void dev_cycle(const Dev &d, int w, int n, const int s[4], double &P, double &Q) {
+    const double t0 = d.cn * double(n), t1 = d.cs0 * double(s[0]), t2 = d.cs1 * double(s[1]),
+                 t3 = d.cs2 * double(s[2]), t4 = d.cs3 * double(s[3]);
+    double a1 = d.r1w * double(w), a2 = d.r2w * double(w);
+    a1 = a1 + t0; a1 = a1 + t1; a1 = a1 + t2; a1 = a1 + t3; a1 = a1 + t4;
+    a2 = a2 + t0; a2 = a2 + t1; a2 = a2 + t2; a2 = a2 + t3; a2 = a2 + t4;
+    P = a1 - d.rhs1;
+    Q = a2 - d.rhs2;
 }
 
-// Best GPU split n for device i holding w layers. The cost is convex
-// piecewise-linear in integer n (every slack is max(lb, affine in n with slope
-// -1/0/+1) and has a non-negative price), so its minimum over the feasible
-// interval sits at an interval end or a kink. Ties -> smallest n.
-__device__ inline bool best_split(const Lds &L, int i, int w, double &g_out, int &n_out, int s_out[4]) {
-    int nL = L.n(DI_NLO, i), nU = L.n(DI_NHI, i);
-    int cand[2 + kRows + 12];
-    int nc = 0;
-    const int nr = L.n(DI_NROW, i);
-    for (int q = 0; q < nr; ++q) {
-        const int *r = L.row(i, q);
-        const int kind = r[0], u = r[1], v = r[2], K = r[3];
-        if (v == 0) continue;
-        if (kind < 0) {  // u w + v n <= K
-            if (v > 0) nU = min(nU, K - u * w); else nL = max(nL, u * w - K);
-        } else {
-            const int slo = L.n(DI_SLO0 + kind, i), shi = L.n(DI_SHI0 + kind, i);
-            if (v > 0) nU = min(nU, shi - K - u * w); else nL = max(nL, u * w + K - shi);
-            cand[nc++] = v * (slo - K - u * w);  // where the slack starts to bind
-            for (int q2 = 0; q2 < q; ++q2) {     // two rows pricing the same slack with opposite slopes
-                const int *r2 = L.row(i, q2);
-                if (r2[0] == kind && r2[2] == -v) {
-                    const int num = (r2[1] * w + r2[3]) - (u * w + K);  // (v - v2) n = num, v - v2 = +-2
-                    const int nn = v > 0 ? num : -num;
-                    const int f = nn >= 0 ? nn / 2 : -((-nn + 1) / 2);
-                    cand[nc++] = f;
-                    cand[nc++] = f + 1;
-                }
-            }
+__device__ inline double least_cycle(const Dev &d, int w, int n, const int s[4]) {
+    double P, Q;
+    dev_cycle(d, w, n, s, P, Q);
+    return Q >= P ? 0.5 * (P + Q) : P;
+}
+
+// Feasible interval of n for w layers (from nlo/nhi, the pure rows and the slack upper bounds).
+__device__ inline void n_interval(const Dev &d, int w, int &nL, int &nU) {
+    nL = d.nlo;
+    nU = d.nhi;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int rest = d.Kf[f] - d.uf[f] * w;  // v n <= rest
+        if (d.vf[f] > 0) nU = min(nU, rest);
+        if (d.vf[f] < 0) nL = max(nL, -rest);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ra = d.shi[j] - d.ua[j] * w - d.Ka[j], rb = d.shi[j] - d.ub[j] * w - d.Kb[j];  // v n <= r
+        if (d.va[j] > 0) nU = min(nU, ra);
+        if (d.va[j] < 0) nL = max(nL, -ra);
+        if (d.vb[j] > 0) nU = min(nU, rb);
+        if (d.vb[j] < 0) nL = max(nL, -rb);
+    }
+}
+
+__device__ inline void try_split(const Dev &d, int w, int nn, int nL, int nU, double &best, int &bn, int bs[4]) {
+    nn = min(max(nn, nL), nU);
+    int s[4];
+    if (least_slacks(d, w, nn, s)) {
+        const double g = dev_cost(d, w, nn, s);
+        if (g < best || (g == best && nn < bn)) {
+            best = g;
+            bn = nn;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bs[j] = s[j];
         }
     }
+}
+
+// Best GPU split n for w layers by full candidate search. The cost is convex
+// piecewise-linear in integer n (each slack is max(lb, affine in n with slope
+// -1/0/+1), prices >= 0), so its minimum over the feasible interval is at an
+// end or at a kink. Ties -> smallest n.
+__device__ inline bool split_full(const Dev &d, int w, double &g, int &n, int s[4]) {
+    int nL, nU;
+    n_interval(d, w, nL, nU);
     if (nL > nU) return false;
     double best = kInf;
     int bn = -1;
-    int bs[4] = {0, 0, 0, 0};
-    cand[nc++] = nL;
-    cand[nc++] = nU;
-    for (int k = 0; k < nc; ++k) {
-        const int nn = min(max(cand[k], nL), nU);
-        int s[4];
-        if (!least_slacks(L, i, w, nn, s)) continue;
-        const double g = dev_cost(L, i, w, nn, s);
-        if (g < best || (g == best && nn < bn)) {
-            best = g; bn = nn;
-            bs[0] = s[0]; bs[1] = s[1]; bs[2] = s[2]; bs[3] = s[3];
-        }
+    try_split(d, w, nL, nL, nU, best, bn, s);
+    try_split(d, w, nU, nL, nU, best, bn, s);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (d.va[j] != 0) try_split(d, w, d.va[j] * (d.slo[j] - d.ua[j] * w - d.Ka[j]), nL, nU, best, bn, s);
+        if (d.vb[j] != 0) try_split(d, w, d.vb[j] * (d.slo[j] - d.ub[j] * w - d.Kb[j]), nL, nU, best, bn, s);
     }
     if (bn < 0) return false;
-    g_out = best; n_out = bn;
-    s_out[0] = bs[0]; s_out[1] = bs[1]; s_out[2] = bs[2]; s_out[3] = bs[3];
+    g = best;
+    n = bn;
     return true;
 }
 
-// Min-plus DP over devices by ONE wave: D[r] = least sum of G over a prefix
-// using r extra layers; choice[i][r] = e taken by device i. With use_T only
-// entries whose cycle time H <= T are allowed. Returns D_M[R].
-__device__ double wave_dp(const Lds &L, int M, int R, bool use_T, double T, int lane) {
-    const int R1 = R + 1;
-    double *D0 = L.D0, *D1 = L.D1;
-    for (int r = lane; r < R1; r += 64) D0[r] = r == 0 ? 0.0 : kInf;
-    wave_sync();
-    for (int i = 0; i < M; ++i) {
-        const double *Gi = L.G + i * R1;
-        const double *Hi = L.H + i * R1;
-        for (int r = lane; r < R1; r += 64) {
-            double best = kInf;
-            int be = 255;
-            for (int e = 0; e <= r; ++e) {
-                const double g = Gi[e];
-                if (use_T && !(Hi[e] <= T)) continue;
-                const double val = D0[r - e] + g;
-                if (val < best) { best = val; be = e; }
+// Incremental step w-1 -> w. The cost is L-natural convex in (w, n) (every term
+// depends on w, n or w - n only; validated at decode), so the least minimiser
+// moves by 0 or +1: only n_prev and n_prev + 1 are candidates.
+__device__ inline bool split_step(const Dev &d, int w, int n_prev, double &g, int &n, int s[4]) {
+    int nL, nU;
+    n_interval(d, w, nL, nU);
+    if (nL > nU) return false;
+    double best = kInf;
+    int bn = -1;
+    try_split(d, w, n_prev, nL, nU, best, bn, s);
+    try_split(d, w, n_prev + 1, nL, nU, best, bn, s);
+    if (bn < 0) return false;
+    g = best;
+    n = bn;
+    return true;
+}
+
+struct WaveCtx {
+    int2 *rows;
+    double *cyc;
+    int *cnt;
+    int *st0, *st1;
+    double *G, *H, *work;
+    uint8_t *split;
+};
+
+__device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, int64_t co, int M, int i, double Wd) {
+    d.cw = B.c[co + i];
+    d.cn = B.c[co + M + i];
+    d.cs0 = B.c[co + 2 * M + i];
+    d.cs1 = B.c[co + 3 * M + i];
+    d.cs2 = B.c[co + 4 * M + i];
+    d.cs3 = B.c[co + 5 * M + i];
+    d.wlo = int(ceil(B.col_lb[co + i]));
+    d.whi = int(floor(fmin(B.col_ub[co + i], Wd)));
+    d.nlo = int(ceil(B.col_lb[co + M + i]));
+    d.nhi = int(floor(fmin(B.col_ub[co + M + i], Wd)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        d.slo[j] = int(ceil(B.col_lb[co + (2 + j) * M + i]));
+        d.shi[j] = int(floor(fmin(B.col_ub[co + (2 + j) * M + i], 1e6)));
+        d.ua[j] = d.va[j] = d.ub[j] = d.vb[j] = 0;
+        d.Ka[j] = d.Kb[j] = kNoRow;
+    }
+    d.uf[0] = d.vf[0] = d.uf[1] = d.vf[1] = 0;
+    d.Kf[0] = d.Kf[1] = 0;
+    d.r1w = w.cyc[4 * i + 0];
+    d.r2w = w.cyc[4 * i + 1];
+    d.rhs1 = w.cyc[4 * i + 2];
+    d.rhs2 = w.cyc[4 * i + 3];
+    const int nrow = w.cnt[i] & 0xff;
+    int nf = 0;
+    int seen[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) {
+        if (q < nrow) {
+            const int2 r = w.rows[i * kRows + q];
+            const int kind = (r.x & 0xff) - 1, u = ((r.x >> 8) & 0xff) - 1, v = ((r.x >> 16) & 0xff) - 1;
+            if (kind < 0) {
+                if (nf == 0) { d.uf[0] = u; d.vf[0] = v; d.Kf[0] = r.y; }
+                else { d.uf[1] = u; d.vf[1] = v; d.Kf[1] = r.y; }
+                ++nf;
             }
-            D1[r] = best;
-            L.choice[i * R1 + r] = uint8_t(be);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (kind == j) {
+                    if (seen[j] == 0) { d.ua[j] = u; d.va[j] = v; d.Ka[j] = r.y; }
+                    else { d.ub[j] = u; d.vb[j] = v; d.Kb[j] = r.y; }
+                    ++seen[j];
+                }
+            }
+        }
+    }
+}
+
+// Tree min-plus DP over the devices. Leaves: A_i[e] = G[i][e] (masked to +inf
+// where H[i][e] > T when use_T). Level l pairs the nodes of level l-1:
+// out_p[r] = min_e L[e] + R[r - e] (argmin e -> split, smallest e on ties);
+// an unpaired last node passes through. Output node p of level l lives in slot
+// p << (l - 1) of `buf` (in place over its left child; buf may be G itself when
+// the leaves are not needed again). Returns the root value at r = R (lane-uniform).
+__device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
+    if (M == 1) {
+        const double g = w.G[R1 - 1];
+        return (use_T && !(w.H[R1 - 1] <= T)) ? kInf : g;
+    }
+    int n = M, l = 0, soff = 0;
+    const int npp = R1 <= 64 ? 64 / R1 : 1;  // output nodes per pass
+    while (n > 1) {
+        const int nout = (n + 1) >> 1;
+        ++l;
+        const double *src = l == 1 ? w.G : buf;
+        const int sh = l == 1 ? 0 : l - 2;  // slot shift of this level's inputs
+        for (int p0 = 0; p0 < nout; p0 += npp) {
+            // each lane: one (node, r) task, or up to 4 states of one node when R1 > 64
+            double best[4] = {kInf, kInf, kInf, kInf};
+            int be[4] = {0, 0, 0, 0}, pp[4] = {-1, -1, -1, -1}, rr[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                int p, r;
+                if (R1 <= 64) {
+                    const int k = lane / R1;
+                    p = p0 + k;
+                    r = lane - k * R1;
+                    if (t > 0 || k >= npp || p >= nout) continue;
+                } else {
+                    p = p0;
+                    r = lane + 64 * t;
+                    if (r >= R1) continue;
+                }
+                pp[t] = p;
+                rr[t] = r;
+                const int a = 2 * p, b = 2 * p + 1;
+                const double *A = src + (int64_t(a) << sh) * RS;
+                if (b < n) {
+                    const double *Bv = src + (int64_t(b) << sh) * RS;
+                    const double *HA = w.H + int64_t(a) * RS, *HB = w.H + int64_t(b) * RS;
+                    for (int e = 0; e <= r; ++e) {
+                        double x = A[e], y = Bv[r - e];
+                        if (l == 1 && use_T) {
+                            if (!(HA[e] <= T)) x = kInf;
+                            if (!(HB[r - e] <= T)) y = kInf;
+                        }
+                        const double v = x + y;
+                        if (v < best[t]) { best[t] = v; be[t] = e; }
+                    }
+                } else {
+                    double x = A[r];
+                    if (l == 1 && use_T && !(w.H[int64_t(a) * RS + r] <= T)) x = kInf;
+                    best[t] = x;
+                    be[t] = r;
+                }
+            }
+            wave_sync();  // every read of this pass before any write
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (pp[t] >= 0) {
+                    buf[(int64_t(pp[t]) << (l - 1)) * RS + rr[t]] = best[t];
+                    w.split[soff + pp[t] * R1 + rr[t]] = uint8_t(be[t]);
+                }
+            }
+            wave_sync();
+        }
+        soff += nout * R1;
+        n = nout;
+    }
+    return buf[R1 - 1];
+}
+
+// Walk the tree top-down from the root state R: st0[i] = e_i of device i.
+__device__ void tree_backtrack(const WaveCtx &w, int M, int R1, int lane) {
+    if (M == 1) {
+        if (lane == 0) w.st0[0] = R1 - 1;
+        wave_sync();
+        return;
+    }
+    // level sizes and split offsets
+    int sizes[12];
+    int offs[12];
+    int L = 0, n = M, soff = 0;
+    while (n > 1) {
+        const int nout = (n + 1) >> 1;
+        sizes[L] = n;  // inputs of level L + 1
+        offs[L] = soff;
+        soff += nout * R1;
+        n = nout;
+        ++L;
+    }
+    int *cur = w.st0, *nxt = w.st1;
+    if (lane == 0) cur[0] = R1 - 1;
+    wave_sync();
+    for (int l = L; l >= 1; --l) {
+        const int nin = sizes[l - 1];
+        const int nout = (nin + 1) >> 1;
+        for (int p = lane; p < nout; p += 64) {
+            const int r = cur[p];
+            const int e = w.split[offs[l - 1] + p * R1 + r];
+            nxt[2 * p] = e;
+            if (2 * p + 1 < nin) nxt[2 * p + 1] = r - e;
         }
         wave_sync();
-        double *t = D0; D0 = D1; D1 = t;
+        int *t = cur; cur = nxt; nxt = t;
     }
-    return D0[R];
-}
-
-// lane 0: walk the choices back; wsol[i] = lb(w_i) + e_i
-__device__ void backtrack(const Lds &L, int M, int R) {
-    const int R1 = R + 1;
-    int r = R;
-    for (int i = M - 1; i >= 0; --i) {
-        const int e = L.choice[i * R1 + r];
-        L.n(DI_WSOL, i) = L.n(DI_WLO, i) + e;
-        r -= e;
+    if (cur != w.st0) {
+        for (int i = lane; i < M; i += 64) w.st0[i] = cur[i];
+        wave_sync();
     }
 }
 
-__global__ __launch_bounds__(kBlock) void halda_solve_kernel(halda_batch B, halda_result Rz, int mmax, int r1max,
-                                                               int tab, int tab_kc) {
+__global__ __launch_bounds__(64) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
+                                                          int mmax, int r1max, int tab, int tab_kc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Layout lay = make_layout(mmax, r1max, tab, tab_kc);
-    Lds L;
-    L.dd = reinterpret_cast<double *>(smem + lay.dd);
-    L.di = reinterpret_cast<int *>(smem + lay.di);
-    L.rows = reinterpret_cast<int *>(smem + lay.rows);
-    L.G = reinterpret_cast<double *>(smem + lay.tab);
-    L.choice = smem + lay.choice;
-    L.D0 = reinterpret_cast<double *>(smem + lay.dp);
-    L.D1 = L.D0 + r1max;
-    L.red = reinterpret_cast<double *>(smem + lay.red);
-    L.sc = reinterpret_cast<int *>(smem + lay.sci);
-    L.mmax = mmax;
+    const int lane = threadIdx.x;
+    const Slice sl = make_slice(mmax, r1max, tab, tab_kc);
+    WaveCtx w;
+    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
+    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
+    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
+    w.st0 = reinterpret_cast<int *>(smem + sl.st0);
+    w.st1 = reinterpret_cast<int *>(smem + sl.st1);
+    w.G = reinterpret_cast<double *>(smem + sl.G);
+    w.H = reinterpret_cast<double *>(smem + sl.H);
+    w.work = reinterpret_cast<double *>(smem + sl.work);
+    w.split = smem + sl.split;
 
-    const int inst = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int N = B.n_cols[inst], m = B.n_rows[inst];
-    const int64_t co = B.col_off[inst], ro = B.row_off[inst];
-    const int32_t *rp = B.row_ptr + B.csr_off[inst];
+    // this wave owns instances blockIdx.x + j * gridDim.x; a 64-wide window of
+    // them is screened by one ballot over cls
+    const int S = gridDim.x;
+    for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
+        const int64_t mine = base + int64_t(lane) * S;
+        const bool open = mine < B.n_inst && cls[mine] != CLS_DONE;
+        uint64_t todo = __ballot(open);
+        while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int inst = int(base + int64_t(bit) * S);
 
-    auto finish = [&](int status) {
-        if (tid == 0) {
-            Rz.status[inst] = status;
-            Rz.nodes[inst] = 0;
-            Rz.obj_lin[inst] = kInf;
-            Rz.dual_bound[inst] = status == HALDA_STATUS_INFEASIBLE ? kInf : -kInf;
-            Rz.gap[inst] = kInf;
-        }
-    };
-    if (N < 1 || (N - 1) % 7 != 0 || m < 1) { finish(HALDA_STATUS_UNSUPPORTED); return; }
-    const int M = (N - 1) / 7, iC = 7 * M;
-    if (M > mmax) { finish(HALDA_STATUS_TOO_LARGE); return; }
+            const int N = B.n_cols[inst], m = B.n_rows[inst];
+            const int M = (N - 1) / 7, iC = 7 * M;
+            const int64_t co = B.col_off[inst], ro = B.row_off[inst];
+            const int32_t *rp = B.row_ptr + B.csr_off[inst];
+            const double Wd = B.row_ub[ro + m - 1];
+            const int W = int(Wd);
+            const double kc = B.c[co + iC];
 
-    if (tid < kScI) L.sc[tid] = 0;
-    __syncthreads();
+            // ---- per-device checks on costs / bounds / integrality; reset row slots
+            int bad = 0, sumlo = 0;
+            for (int i = lane; i < M; i += 64) {
+                for (int b = 0; b < 6; ++b) bad |= B.integrality[co + b * M + i] != 1;
+                bad |= B.integrality[co + 6 * M + i] != 0 || B.c[co + 6 * M + i] != 0.0;
+                bad |= B.col_lb[co + 6 * M + i] != 0.0 || B.col_ub[co + 6 * M + i] != kInf;
+                bad |= B.col_lb[co + M + i] < 0.0;
+                for (int j = 0; j < 4; ++j) bad |= !(B.c[co + (2 + j) * M + i] >= 0.0);
+                sumlo += int(ceil(B.col_lb[co + i]));
+                w.cnt[i] = 0;
+            }
+            if (lane == 0)
+                bad |= !(kc >= 0.0) || B.integrality[co + iC] != 0 || B.col_lb[co + iC] != 0.0 ||
+                       B.col_ub[co + iC] != kInf;
+            sumlo = wave_sum(sumlo);
+            const int R1 = W - sumlo + 1, RS = odd_stride(R1);
+            wave_sync();
 
-    // ---- equality row sum_i w_i = W and quick bound infeasibility
-    const double Wd = B.row_ub[ro + m - 1];
-    const int eqs = rp[m - 1], eqe = rp[m];
-    if (!(B.row_lb[ro + m - 1] == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M) {
-        finish(HALDA_STATUS_UNSUPPORTED);
-        return;
-    }
-    const int W = int(Wd);
-    for (int i = tid; i < M; i += kBlock) {
-        if (B.col_idx[eqs + i] != i || B.val[eqs + i] != 1.0) atomicOr(&L.sc[SC_FLAGS], F_UNSUPPORTED);
-        const double lb = B.col_lb[co + i], ub = B.col_ub[co + i];
-        const int wlo = int(ceil(lb)), whi = int(floor(fmin(ub, Wd)));
-        L.n(DI_WLO, i) = wlo;
-        L.n(DI_WHI, i) = whi;
-        atomicAdd(&L.sc[SC_SUMWLO], wlo);
-        if (wlo > whi || lb < 0.0) atomicOr(&L.sc[SC_FLAGS], F_INFEASIBLE);
-    }
-    __syncthreads();
-    {
-        const int fl = L.sc[SC_FLAGS];
-        if (fl & F_UNSUPPORTED) { finish(HALDA_STATUS_UNSUPPORTED); return; }
-        if ((fl & F_INFEASIBLE) || L.sc[SC_SUMWLO] > W) { finish(HALDA_STATUS_INFEASIBLE); return; }
-    }
-    const int R = W - L.sc[SC_SUMWLO];
-    const int R1 = R + 1;
-    const double kc = B.c[co + iC];
-    if (R1 > r1max || M * R1 > (kc > 0.0 ? tab_kc : tab)) { finish(HALDA_STATUS_TOO_LARGE); return; }
-    L.H = L.G + M * R1;
-
-    // ---- per-device costs and bounds
-    for (int i = tid; i < M; i += kBlock) {
-        int bad = 0;
-        const double cw = B.c[co + i], cn = B.c[co + M + i];
-        L.d(DD_CW, i) = cw;
-        L.d(DD_CN, i) = cn;
-        for (int b = 0; b < 6; ++b) bad |= B.integrality[co + b * M + i] != 1;
-        bad |= B.integrality[co + 6 * M + i] != 0 || B.c[co + 6 * M + i] != 0.0;
-        bad |= B.col_lb[co + 6 * M + i] != 0.0 || B.col_ub[co + 6 * M + i] != kInf;
-        const double nlo = B.col_lb[co + M + i], nhi = B.col_ub[co + M + i];
-        L.n(DI_NLO, i) = int(ceil(nlo));
-        L.n(DI_NHI, i) = int(floor(fmin(nhi, Wd)));
-        for (int s = 0; s < 4; ++s) {
-            const double cs = B.c[co + (2 + s) * M + i];
-            L.d(DD_CS0 + s, i) = cs;
-            bad |= !(cs >= 0.0);
-            L.n(DI_SLO0 + s, i) = int(ceil(B.col_lb[co + (2 + s) * M + i]));
-            L.n(DI_SHI0 + s, i) = int(floor(fmin(B.col_ub[co + (2 + s) * M + i], 1e6)));
-        }
-        bad |= nlo < 0.0;
-        L.n(DI_NROW, i) = 0;
-        L.n(DI_HAVE1, i) = 0;
-        L.n(DI_HAVE2, i) = 0;
-        if (bad) atomicOr(&L.sc[SC_FLAGS], F_UNSUPPORTED);
-    }
-    if (tid == 0) {
-        const bool ok = kc >= 0.0 && B.integrality[co + iC] == 0 && B.col_lb[co + iC] == 0.0 &&
-                        B.col_ub[co + iC] == kInf;
-        if (!ok) atomicOr(&L.sc[SC_FLAGS], F_UNSUPPORTED);
-    }
-    __syncthreads();
-
-    // ---- rows: classify by nonzero pattern (one thread per row)
-    for (int r = tid; r < m - 1; r += kBlock) {
-        const int s = rp[r], e = rp[r + 1], nnz = e - s;
-        const double rhs = B.row_ub[ro + r];
-        int bad = B.row_lb[ro + r] != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs) < 1e300);
-        int cols[kMaxRowNnz];
-        double vals[kMaxRowNnz];
-        for (int k = 0; k < kMaxRowNnz; ++k) {
-            if (!bad && k < nnz) { cols[k] = B.col_idx[s + k]; vals[k] = B.val[s + k]; }
-        }
-        if (!bad && cols[nnz - 1] == iC) {
-            // cycle row: busy(i) +- z_i - C <= rhs
-            const int zc = nnz >= 2 ? cols[nnz - 2] : -1;
-            const int dev = zc - 6 * M;
-            bad |= vals[nnz - 1] != -1.0 || dev < 0 || dev >= M || fabs(vals[nnz - 2]) != 1.0;
-            if (!bad) {
-                const bool first = vals[nnz - 2] > 0.0;
-                double coef[6] = {0, 0, 0, 0, 0, 0};
-                for (int k = 0; k < nnz - 2; ++k) {
-                    const int j = cols[k];
-                    if (j >= 6 * M || j % M != dev) { bad = 1; break; }
-                    coef[j / M] = vals[k];
+            // ---- rows: classify by nonzero pattern (lane-strided, two rows per lane in flight)
+            for (int r0 = 0; r0 < m - 1; r0 += 128) {
+                int rs[2], re[2];
+                double rhs[2], rlb[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int r = r0 + 64 * h + lane;
+                    const bool in = r < m - 1;
+                    rs[h] = in ? rp[r] : 0;
+                    re[h] = in ? rp[r + 1] : 0;
+                    rhs[h] = in ? B.row_ub[ro + r] : 0.0;
+                    rlb[h] = in ? B.row_lb[ro + r] : -kInf;
                 }
-                // the non-w part of a cycle row must equal the device's objective terms
-                bad |= coef[1] != L.d(DD_CN, dev);
-                for (int b = 0; b < 4; ++b) bad |= coef[2 + b] != L.d(DD_CS0 + b, dev);
-                if (!bad) {
-                    if (first) {
-                        L.d(DD_R1W, dev) = coef[0]; L.d(DD_RHS1, dev) = rhs;
-                        atomicAdd(&L.n(DI_HAVE1, dev), 1);
-                    } else {
-                        L.d(DD_R2W, dev) = coef[0]; L.d(DD_RHS2, dev) = rhs;
-                        atomicAdd(&L.n(DI_HAVE2, dev), 1);
+                int cols[2][kMaxRowNnz];
+                double vals[2][kMaxRowNnz];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int nnz = re[h] - rs[h];
+#pragma unroll
+                    for (int k = 0; k < kMaxRowNnz; ++k) {
+                        const bool in = k < nnz;
+                        cols[h][k] = in ? B.col_idx[rs[h] + k] : -1;
+                        vals[h][k] = in ? B.val[rs[h] + k] : 0.0;
                     }
                 }
-            }
-        } else if (!bad) {
-            // capacity / link row of one device: aw w + an n - beta s <= rhs
-            int dev = -1, slack = -1;
-            double aw = 0.0, an = 0.0, beta = 0.0;
-            for (int k = 0; k < nnz; ++k) {
-                const int j = cols[k], blk = j / M, i = j % M;
-                if (j >= 6 * M || (dev >= 0 && i != dev)) { bad = 1; break; }
-                dev = i;
-                if (blk == 0) aw = vals[k];
-                else if (blk == 1) an = vals[k];
-                else if (slack >= 0) { bad = 1; break; }
-                else { slack = blk - 2; beta = -vals[k]; }
-            }
-            int u = 0, v = 0, K = 0;
-            if (!bad) {
-                const double scale = slack >= 0 ? beta : fmax(fabs(aw), fabs(an));
-                bad |= !(scale > 0.0);
-                if (!bad) {
-                    bad |= !(aw == 0.0 || fabs(aw) == scale) || !(an == 0.0 || fabs(an) == scale);
-                    u = aw == 0.0 ? 0 : (aw > 0.0 ? 1 : -1);
-                    v = an == 0.0 ? 0 : (an > 0.0 ? 1 : -1);
-                    double kk;
-                    if (slack >= 0) kk = ceil(-rhs / beta - kSlackEps);
-                    else kk = floor((rhs + kSlackEps * fmax(1.0, fabs(rhs))) / scale);
-                    bad |= !(fabs(kk) < 1e8);
-                    K = int(kk);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int r = r0 + 64 * h + lane;
+                    if (r >= m - 1) continue;
+                    const int nnz = re[h] - rs[h];
+                    int rb = rlb[h] != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs[h]) < 1e300);
+                    if (rb) { bad = 1; continue; }
+                    int last = -1, zc = -1;
+                    double vlast = 0.0, vz = 0.0;
+#pragma unroll
+                    for (int k = 0; k < kMaxRowNnz; ++k) {
+                        if (k == nnz - 1) { last = cols[h][k]; vlast = vals[h][k]; }
+                        if (k == nnz - 2) { zc = cols[h][k]; vz = vals[h][k]; }
+                    }
+                    if (last == iC) {
+                        // cycle row: busy(i) +- z_i - C <= rhs; its non-w part must equal the objective's
+                        const int dev = zc - 6 * M;
+                        rb |= vlast != -1.0 || nnz < 2 || dev < 0 || dev >= M || fabs(vz) != 1.0;
+                        double coef[6] = {0, 0, 0, 0, 0, 0};
+                        if (!rb) {
+#pragma unroll
+                            for (int k = 0; k < kMaxRowNnz; ++k) {
+                                if (k < nnz - 2) {
+                                    const int j = cols[h][k];
+                                    if (j >= 6 * M || j % M != dev) rb = 1;
+                                    else {
+                                        const int blk = j / M;
+#pragma unroll
+                                        for (int b = 0; b < 6; ++b)
+                                            if (blk == b) coef[b] = vals[h][k];
+                                    }
+                                }
+                            }
+                        }
+                        if (!rb) {
+#pragma unroll
+                            for (int b = 1; b < 6; ++b) rb |= coef[b] != B.c[co + b * M + dev];
+                        }
+                        if (!rb) {
+                            const bool first = vz > 0.0;
+                            w.cyc[4 * dev + (first ? 0 : 1)] = coef[0];
+                            w.cyc[4 * dev + (first ? 2 : 3)] = rhs[h];
+                            atomicAdd(&w.cnt[dev], first ? (1 << 8) : (1 << 16));
+                        }
+                    } else {
+                        // capacity / link row of one device: aw w + an n - beta s <= rhs
+                        int dev = -1, slack = -1;
+                        double aw = 0.0, an = 0.0, beta = 0.0;
+#pragma unroll
+                        for (int k = 0; k < kMaxRowNnz; ++k) {
+                            if (k < nnz) {
+                                const int j = cols[h][k], blk = j / M, i = j % M;
+                                if (j >= 6 * M || (dev >= 0 && i != dev)) rb = 1;
+                                dev = i;
+                                if (blk == 0) aw = vals[h][k];
+                                else if (blk == 1) an = vals[h][k];
+                                else if (slack >= 0) rb = 1;
+                                else { slack = blk - 2; beta = -vals[h][k]; }
+                            }
+                        }
+                        const double scale = slack >= 0 ? beta : fmax(fabs(aw), fabs(an));
+                        rb |= !(scale > 0.0) || !(aw == 0.0 || fabs(aw) == scale) ||
+                              !(an == 0.0 || fabs(an) == scale);
+                        const int u = aw == 0.0 ? 0 : (aw > 0.0 ? 1 : -1);
+                        const int v = an == 0.0 ? 0 : (an > 0.0 ? 1 : -1);
+                        // L-natural convexity: a row may couple w and n only through w - n
+                        rb |= u * v > 0;
+                        if (!rb) {
+                            const double kk = slack >= 0
+                                                  ? ceil(-rhs[h] / beta - kSlackEps)
+                                                  : floor((rhs[h] + kSlackEps * fmax(1.0, fabs(rhs[h]))) / scale);
+                            rb |= !(fabs(kk) < 1e8);
+                            if (!rb) {
+                                const int q = atomicAdd(&w.cnt[dev], 1) & 0xff;
+                                if (q >= kRows) rb = 1;
+                                else
+                                    w.rows[dev * kRows + q] =
+                                        make_int2((slack + 1) | ((u + 1) << 8) | ((v + 1) << 16), int(kk));
+                            }
+                        }
+                    }
+                    bad |= rb;
                 }
             }
-            if (!bad) {
-                const int q = atomicAdd(&L.n(DI_NROW, dev), 1);
-                if (q >= kRows) bad = 1;
-                else {
-                    int *rw = L.row(dev, q);
-                    rw[0] = slack; rw[1] = u; rw[2] = v; rw[3] = K;
-                }
-            }
-        }
-        if (bad) atomicOr(&L.sc[SC_FLAGS], F_UNSUPPORTED);
-    }
-    __syncthreads();
-    for (int i = tid; i < M; i += kBlock)
-        if (L.n(DI_HAVE1, i) != 1 || L.n(DI_HAVE2, i) != 1 || L.n(DI_NROW, i) > kRows)
-            atomicOr(&L.sc[SC_FLAGS], F_UNSUPPORTED);
-    __syncthreads();
-    if (L.sc[SC_FLAGS] & F_UNSUPPORTED) { finish(HALDA_STATUS_UNSUPPORTED); return; }
-
-    // ---- table phase: G[i][e], H[i][e] for w = lb(w_i) + e
-    for (int p = tid; p < M * R1; p += kBlock) {
-        const int i = p / R1, e = p - i * R1;
-        const int w = L.n(DI_WLO, i) + e;
-        double g = kInf, h = kInf;
-        int n, s[4];
-        if (w <= L.n(DI_WHI, i) && best_split(L, i, w, g, n, s)) {
-            if (kc > 0.0) {
-                double P, Q;
-                dev_cycle(L, i, w, n, s, P, Q);
-                h = fmax(0.0, Q >= P ? 0.5 * (P + Q) : P);
-            }
-        } else {
-            g = kInf;
-        }
-        L.G[p] = g;
-        if (kc > 0.0) L.H[p] = h;
-    }
-    __syncthreads();
-
-    // ---- DP (wave 0); k > 1: ascending threshold scan with bound pruning
-    if (wave == 0) {
-        int nodes = 1;
-        const double s_inf = wave_dp(L, M, R, false, 0.0, lane);
-        int status = s_inf < kInf ? HALDA_STATUS_OPTIMAL : HALDA_STATUS_INFEASIBLE;
-        if (status == HALDA_STATUS_OPTIMAL && kc > 0.0) {
-            if (lane == 0) backtrack(L, M, R);
             wave_sync();
-            double hmax = 0.0;
-            for (int i = lane; i < M; i += 64) hmax = fmax(hmax, L.H[i * R1 + (L.n(DI_WSOL, i) - L.n(DI_WLO, i))]);
-            hmax = wave_max(hmax);
-            double best = kc * hmax + s_inf, bestT = kInf;
-            // every assignment has max_i H_i >= T_lo = max_i min_e H[i][e]
-            double tlo = 0.0;
+            // every device: one row of each cycle kind, <= 2 rows per slack, <= 2 pure rows
             for (int i = lane; i < M; i += 64) {
-                double mn = kInf;
-                for (int e = 0; e < R1; ++e)
-                    if (L.G[i * R1 + e] < kInf) mn = fmin(mn, L.H[i * R1 + e]);
-                tlo = fmax(tlo, mn);
-            }
-            tlo = wave_max(tlo);
-            double tprev = -1.0;
-            while (true) {
-                double t = kInf;
-                for (int p = lane; p < M * R1; p += 64) {
-                    const double h = L.H[p];
-                    if (L.G[p] < kInf && h >= tlo && h > tprev) t = fmin(t, h);
+                const int c = w.cnt[i], nr = min(c & 0xff, kRows);
+                bad |= (c & 0xff) > kRows || ((c >> 8) & 0xff) != 1 || ((c >> 16) & 0xff) != 1;
+                int per[5] = {0, 0, 0, 0, 0};
+                for (int q = 0; q < nr; ++q) {
+                    const int kind = (w.rows[i * kRows + q].x & 0xff) - 1;
+                    for (int j = 0; j < 5; ++j) per[j] += (kind == j - 1);
                 }
-                t = wave_min(t);
-                if (!(t < kInf) || kc * t + s_inf >= best) break;
-                const double st = wave_dp(L, M, R, true, t, lane);
-                ++nodes;
-                if (st < kInf && kc * t + st < best) { best = kc * t + st; bestT = t; }
-                tprev = t;
+                for (int j = 0; j < 5; ++j) bad |= per[j] > 2;
             }
-            if (bestT < kInf) wave_dp(L, M, R, true, bestT, lane);
-            else wave_dp(L, M, R, false, 0.0, lane);
-            ++nodes;
-        }
-        if (lane == 0) {
-            if (status == HALDA_STATUS_OPTIMAL) backtrack(L, M, R);
-            L.sc[SC_STATUS] = status;
-            L.sc[SC_NODES] = nodes;
-        }
-    }
-    __syncthreads();
-    if (L.sc[SC_STATUS] != HALDA_STATUS_OPTIMAL) {
-        if (tid == 0) {
-            Rz.status[inst] = L.sc[SC_STATUS];
-            Rz.nodes[inst] = L.sc[SC_NODES];
-            Rz.obj_lin[inst] = kInf;
-            Rz.dual_bound[inst] = kInf;
-            Rz.gap[inst] = kInf;
-        }
-        return;
-    }
+            bad = wave_or(bad);
+            if (bad) {
+                if (lane == 0) write_done(Rz, inst, HALDA_STATUS_UNSUPPORTED, 0);
+                continue;
+            }
 
-    // ---- rebuild x for the chosen w: n, least slacks, stall z, cycle time C
-    for (int i = tid; i < M; i += kBlock) {
-        const int w = L.n(DI_WSOL, i);
-        double g = 0.0, P, Q;
-        int n = 0, s[4] = {0, 0, 0, 0};
-        best_split(L, i, w, g, n, s);
-        dev_cycle(L, i, w, n, s, P, Q);
-        double *x = Rz.x + co;
-        x[i] = double(w);
-        x[M + i] = double(n);
-        x[2 * M + i] = double(s[0]);
-        x[3 * M + i] = double(s[1]);
-        x[4 * M + i] = double(s[2]);
-        x[5 * M + i] = double(s[3]);
-        x[6 * M + i] = Q > P ? 0.5 * (Q - P) : 0.0;
-        L.d(DD_G, i) = g;
-        L.d(DD_H, i) = Q >= P ? 0.5 * (P + Q) : P;
-    }
-    __syncthreads();
-    if (wave == 0) {
-        double h = 0.0;
-        for (int i = lane; i < M; i += 64) h = fmax(h, L.d(DD_H, i));
-        h = wave_max(h);
-        if (lane == 0) {
-            double obj = 0.0;
-            for (int i = 0; i < M; ++i) obj = obj + L.d(DD_G, i);
-            obj = obj + kc * h;
-            Rz.x[co + iC] = h;
-            Rz.status[inst] = HALDA_STATUS_OPTIMAL;
-            Rz.obj_lin[inst] = obj;
-            Rz.dual_bound[inst] = obj;
-            Rz.gap[inst] = 0.0;
-            Rz.nodes[inst] = L.sc[SC_NODES];
+            // ---- tables: lane = device, e = 0..R: G[i][e], H[i][e]
+            for (int i = lane; i < M; i += 64) {
+                Dev d;
+                load_dev(d, B, w, co, M, i, Wd);
+                int n = 0, s[4];
+                bool have = false;
+                for (int e = 0; e < R1; ++e) {
+                    const int wl = d.wlo + e;
+                    double g = kInf, h = kInf;
+                    bool ok = false;
+                    if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
+                    if (ok && kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
+                    have = ok;
+                    w.G[i * RS + e] = ok ? g : kInf;
+                    if (kc > 0.0) w.H[i * RS + e] = h;
+                }
+            }
+            wave_sync();
+
+            // ---- DP; k > 1: ascending threshold scan with bound pruning. One call
+            // site: phase 0 = unconstrained, 1 = threshold scan, 2 = final re-run.
+            double *buf = kc > 0.0 ? w.work : w.G;
+            int64_t nodes = 0;
+            int phase = 0;
+            bool use_T = false, feasible = true;
+            double T = 0.0, s_inf = kInf, best = kInf, bestT = kInf, tprev = -1.0, tlo = 0.0;
+            while (true) {
+                const double st = tree_dp(w, M, R1, RS, use_T, T, buf, lane);
+                ++nodes;
+                if (phase == 2) break;
+                if (phase == 0) {
+                    s_inf = st;
+                    if (!(st < kInf)) { feasible = false; break; }
+                    if (!(kc > 0.0)) break;  // k = 1: the splits of this pass are final
+                    tree_backtrack(w, M, R1, lane);
+                    double hmax = 0.0;
+                    for (int i = lane; i < M; i += 64) {
+                        hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
+                        double mn = kInf;
+                        for (int e = 0; e < R1; ++e)
+                            if (w.G[i * RS + e] < kInf) mn = fmin(mn, w.H[i * RS + e]);
+                        tlo = fmax(tlo, mn);  // every assignment has max_i H_i >= max_i min_e H[i][e]
+                    }
+                    hmax = wave_max(hmax);
+                    tlo = wave_max(tlo);
+                    best = kc * hmax + s_inf;
+                    phase = 1;
+                } else if (st < kInf && kc * T + st < best) {
+                    best = kc * T + st;
+                    bestT = T;
+                }
+                if (phase == 1) {
+                    if (use_T) tprev = T;
+                    double t = kInf;
+                    for (int i = lane; i < M; i += 64)
+                        for (int e = 0; e < R1; ++e) {
+                            const double h = w.H[i * RS + e];
+                            if (w.G[i * RS + e] < kInf && h >= tlo && h > tprev) t = fmin(t, h);
+                        }
+                    t = wave_min(t);
+                    if (t < kInf && kc * t + s_inf < best) {
+                        use_T = true;
+                        T = t;
+                        continue;
+                    }
+                    if (!use_T && !(bestT < kInf)) break;  // no scan pass ran: phase-0 splits are final
+                    phase = 2;
+                    use_T = bestT < kInf;
+                    T = bestT;
+                }
+            }
+            if (!feasible) {
+                if (lane == 0) write_done(Rz, inst, HALDA_STATUS_INFEASIBLE, nodes);
+                continue;
+            }
+            tree_backtrack(w, M, R1, lane);
+
+            // ---- rebuild x for the chosen w: n, least slacks, stall z, cycle time C
+            double hmax = 0.0;
+            for (int i = lane; i < M; i += 64) {
+                Dev d;
+                load_dev(d, B, w, co, M, i, Wd);
+                const int wl = d.wlo + w.st0[i];
+                double g = 0.0, P, Q;
+                int n = 0, s[4] = {0, 0, 0, 0};
+                split_full(d, wl, g, n, s);
+                dev_cycle(d, wl, n, s, P, Q);
+                double *x = Rz.x + co;
+                x[i] = double(wl);
+                x[M + i] = double(n);
+                x[2 * M + i] = double(s[0]);
+                x[3 * M + i] = double(s[1]);
+                x[4 * M + i] = double(s[2]);
+                x[5 * M + i] = double(s[3]);
+                x[6 * M + i] = Q > P ? 0.5 * (Q - P) : 0.0;
+                w.cyc[4 * i] = g;  // per-device cost scratch for the ordered sum below
+                hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
+            }
+            hmax = wave_max(hmax);
+            wave_sync();
+            if (lane == 0) {
+                double gsum = 0.0;
+                for (int i = 0; i < M; ++i) gsum = gsum + w.cyc[4 * i];
+                const double obj = gsum + kc * hmax;
+                Rz.x[co + iC] = hmax;
+                Rz.status[inst] = HALDA_STATUS_OPTIMAL;
+                Rz.obj_lin[inst] = obj;
+                Rz.dual_bound[inst] = obj;
+                Rz.gap[inst] = 0.0;
+                Rz.nodes[inst] = nodes;
+            }
+            wave_sync();
         }
     }
 }
@@ -544,37 +770,65 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                                   \
-    do {                                                                                                \
-        hipError_t e_ = (expr);                                                                         \
+#define HIP_TRY(expr)                                                                                       \
+    do {                                                                                                    \
+        hipError_t e_ = (expr);                                                                             \
         if (e_ != hipSuccess) return fail(HALDA_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
 struct Ctx {
     int device = 0;
+    int cus = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr;  // launch start, end, solve-kernel start
     bool timed = false;
-    void *scratch = nullptr;
+    void *scratch = nullptr;  // host-API staging
     size_t scratch_bytes = 0;
+    void *work = nullptr;  // cls[n]: screen verdict per instance
+    size_t work_bytes = 0;
 };
 
-int64_t lds_for(int mmax, int r1max, int tab, int tab_kc) { return make_layout(mmax, r1max, tab, tab_kc).total; }
+int64_t slice_bytes_for(int mmax, int r1max, int tab, int tab_kc) {
+    return make_slice(mmax, r1max, tab, tab_kc).total;
+}
 
 int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t stream) {
     if (in.n_inst <= 0) return HALDA_OK;
     if (in.max_cols < 1 || in.max_R1 < 1 || in.max_tab < 0 || in.max_tab_kc < 0)
         return fail(HALDA_E_ARG, "halda_batch shape summary (max_cols/max_R1/max_tab/max_tab_kc) not set");
+    if (in.max_R1 > 256) return fail(HALDA_E_ARG, "max_R1 > 256 (W - sum lb(w) must be < 256)");
     const int mmax = (in.max_cols - 1) / 7 + 1;
-    const int tab = in.max_tab > 0 ? in.max_tab : 1, tab_kc = in.max_tab_kc;
-    const int64_t lds = lds_for(mmax, in.max_R1, tab, tab_kc);
+    // table sizes in doubles with the odd row stride used on chip
+    // M * RS <= M * (R + 1) + M: the odd row stride costs at most one double per device
+    const int64_t tab = std::max<int64_t>(1, in.max_tab > 0 ? int64_t(in.max_tab) + mmax : 0);
+    const int64_t tab_kc = in.max_tab_kc > 0 ? int64_t(in.max_tab_kc) + mmax : 0;
+    if (tab > (1 << 24) || tab_kc > (1 << 24)) return fail(HALDA_E_ARG, "table summary out of range");
+    const int64_t lds = slice_bytes_for(mmax, in.max_R1, int(tab), int(tab_kc));
     if (lds > 160 * 1024)
-        return fail(HALDA_E_ARG, "batch needs " + std::to_string(lds) + " B of LDS per instance (> 160 KiB)");
+        return fail(HALDA_E_ARG, "batch needs " + std::to_string(lds) + " B of LDS per solve wave (> 160 KiB)");
+    const size_t n = size_t(in.n_inst);
+    if (n > ctx->work_bytes) {
+        if (ctx->work) HIP_TRY(hipFree(ctx->work));
+        ctx->work = nullptr;
+        ctx->work_bytes = 0;
+        HIP_TRY(hipMalloc(&ctx->work, (n + 255) & ~size_t(255)));
+        ctx->work_bytes = (n + 255) & ~size_t(255);
+    }
+    uint8_t *cls = static_cast<uint8_t *>(ctx->work);
+    HIP_TRY(hipEventRecord(ctx->ev0, stream));
+    hipLaunchKernelGGL(halda_screen_kernel, dim3((in.n_inst + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0,
+                       stream, in, out, cls, mmax, in.max_R1, int(tab), int(tab_kc));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->evs, stream));
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(halda_solve_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-    HIP_TRY(hipEventRecord(ctx->ev0, stream));
-    hipLaunchKernelGGL(halda_solve_kernel, dim3(in.n_inst), dim3(kBlock), size_t(lds), stream, in, out, mmax,
-                       in.max_R1, tab, tab_kc);
+    // persistent grid: exactly the resident capacity (one 64-thread workgroup = one wave)
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, halda_solve_kernel, 64, size_t(lds)));
+    per_cu = std::max(1, per_cu);
+    const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
+    hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds), stream, in, out, cls, mmax,
+                       in.max_R1, int(tab), int(tab_kc));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
@@ -588,14 +842,16 @@ extern "C" {
 int halda_version(void) { return HALDA_ABI_VERSION; }
 
 int halda_last_error(char *buf, size_t len) {
-    if (buf && len) {
-        std::snprintf(buf, len, "%s", g_err.c_str());
-    }
+    if (buf && len) std::snprintf(buf, len, "%s", g_err.c_str());
     return int(g_err.size());
 }
 
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc) {
-    return lds_for((max_cols - 1) / 7 + 1, max_R1, max_tab > 0 ? max_tab : 1, max_tab_kc);
+    if (max_R1 < 1 || max_R1 > 256) return -1;
+    const int mmax = (max_cols - 1) / 7 + 1;
+    const int64_t tab = std::max<int64_t>(1, max_tab > 0 ? int64_t(max_tab) + mmax : 0);
+    const int64_t tab_kc = max_tab_kc > 0 ? int64_t(max_tab_kc) + mmax : 0;
+    return slice_bytes_for(mmax, max_R1, int(tab), int(tab_kc));
 }
 
 int halda_init(int device_ordinal, void **ctx_out) {
@@ -612,8 +868,10 @@ int halda_init(int device_ordinal, void **ctx_out) {
     HIP_TRY(hipSetDevice(device_ordinal));
     Ctx *c = new Ctx();
     c->device = device_ordinal;
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->evs) != hipSuccess) {
         delete c;
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
@@ -626,8 +884,10 @@ void halda_free(void *ctx) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->work) (void)hipFree(c->work);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->evs) (void)hipEventDestroy(c->evs);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -651,6 +911,17 @@ int halda_last_kernel_ms(void *ctx, double *ms) {
     return HALDA_OK;
 }
 
+int halda_last_solve_kernel_ms(void *ctx, double *ms) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !ms) return fail(HALDA_E_ARG, "NULL ctx/ms");
+    if (!c->timed) return fail(HALDA_E_ARG, "no solve has been launched on this context");
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float f = 0.f;
+    HIP_TRY(hipEventElapsedTime(&f, c->evs, c->ev1));
+    *ms = f;
+    return HALDA_OK;
+}
+
 int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c || !in_h || !out_h) return fail(HALDA_E_ARG, "NULL ctx/in/out");
@@ -663,7 +934,6 @@ int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
         return fail(HALDA_E_ARG, "halda_batch has a NULL array");
     if (!out_h->status || !out_h->x || !out_h->obj_lin || !out_h->dual_bound || !out_h->gap || !out_h->nodes)
         return fail(HALDA_E_ARG, "halda_result has a NULL array");
-    // extents of the shared arrays
     int64_t n_colsum = 0, n_rowsum = 0, n_rp = 0, nnz = 0;
     halda_batch d = h;
     const bool need_summary = h.max_cols == 0 && h.max_R1 == 0 && h.max_tab == 0 && h.max_tab_kc == 0;
@@ -694,7 +964,6 @@ int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
         }
     }
     HIP_TRY(hipSetDevice(c->device));
-    // one grow-only device allocation, 256-B aligned sub-buffers
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_ncols = take(4 * n), o_nrows = take(4 * n), o_csr = take(8 * n), o_col = take(8 * n),

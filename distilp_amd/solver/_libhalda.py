@@ -75,7 +75,7 @@ class HaldaResultC(ctypes.Structure):
 
 
 EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
-           "halda_lds_bytes", "halda_last_error", "halda_free")
+           "halda_last_solve_kernel_ms", "halda_lds_bytes", "halda_last_error", "halda_free")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -102,6 +102,8 @@ def load_library(path: Path | str | None = None):
         lib.halda_solve_batch_device.restype = ctypes.c_int
         lib.halda_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.halda_last_kernel_ms.restype = ctypes.c_int
+        lib.halda_last_solve_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        lib.halda_last_solve_kernel_ms.restype = ctypes.c_int
         lib.halda_lds_bytes.argtypes = [ctypes.c_int32] * 4
         lib.halda_lds_bytes.restype = ctypes.c_int64
         lib.halda_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
@@ -238,9 +240,11 @@ class HaldaContext:
         if rc != 0:
             raise RuntimeError(f"halda_solve_batch_device failed ({rc}): {last_error(self.lib)}")
 
-    def last_kernel_ms(self) -> float:
+    def last_kernel_ms(self, solve_only: bool = False) -> float:
+        """Device time of the last launch sequence (or of halda_solve_kernel alone)."""
         ms = ctypes.c_double()
-        rc = self.lib.halda_last_kernel_ms(self.ctx, ctypes.byref(ms))
+        fn = self.lib.halda_last_solve_kernel_ms if solve_only else self.lib.halda_last_kernel_ms
+        rc = fn(self.ctx, ctypes.byref(ms))
         if rc != 0:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value

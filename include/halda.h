@@ -112,8 +112,11 @@ int halda_solve_batch(void *ctx, const halda_batch *in, halda_result *out);
  * enqueued on `stream` (a hipStream_t; NULL = the context's stream). */
 int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out, void *stream);
 
-/* Device time of the last solve's kernel(s) in ms (valid after the stream is synchronised). */
+/* Device time of the last solve's kernel sequence (screen + compact + solve) in ms. */
 int halda_last_kernel_ms(void *ctx, double *ms);
+
+/* Device time of the last solve's main kernel (halda_solve_kernel) alone, in ms. */
+int halda_last_solve_kernel_ms(void *ctx, double *ms);
 
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Profiling recipe used for profiles/<round>_*: run on the GPU box from the repo root.
+#   bash profiles/run_profile.sh r01
+# 1) rocprofv3 kernel trace + stats of the bench (same command as the bench line, fewer steps)
+# 2) two separate PMC passes (FETCH_SIZE, WRITE_SIZE) with kernel trace only, per MI355X_MICROARCH.md
+set -euo pipefail
+R=${1:-r01}
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_$R
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
+timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_write" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
