@@ -172,3 +172,16 @@ def test_debug_output_format(llama_online_model, capsys):
     assert out[0] == "Objectives by k"
     assert out[1] == "k: 1" and out[2].startswith("  k=1     obj=")
     assert out[-1] == "  k=80    obj=infeasible"
+
+
+def test_host_api_computes_shape_summary_itself(llama_online_model):
+    """INTEGRATION.md path B: one scipy-style MILP, shape summary left at 0."""
+    import dataclasses
+
+    devs = synth_devices(8, 3)
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    batch, refs = assemble([fl], [[1, 2, 4, 5]])
+    auto = dataclasses.replace(batch, max_cols=0, max_R1=0, max_tab=0, max_tab_kc=0)
+    a = get_context(0).solve(batch)
+    b = get_context(0).solve(auto)
+    assert np.array_equal(a.status, b.status) and np.array_equal(a.x, b.x)
