@@ -52,14 +52,16 @@ enum { CLS_DONE = 0, CLS_K1 = 1, CLS_KC = 2 };  // screen verdicts
 // One solve wave = one 64-thread workgroup with its own LDS slice (bytes):
 //   rows   per device kRows x int2 {pack(kind + 1, u + 1, v + 1), K}
 //   cyc    per device {r1w, r2w, rhs1, rhs2} (cycle-row w coefficients and rhs)
+//   cost   per device objective entries {cw, cn, cs0..cs3}
 //   cnt    per device row counter | have1 << 8 | have2 << 16
 //   st0/1  per device ints (DP backtracking states, ping-pong)
+//   rng    per DP-tree slot: finite range [lo, hi] of the node's sequence
 //   G      [i][e] table, row stride RS (odd), leaves of the DP tree; k = 1 reduces in place
 //   H      [i][e] least cycle time (k > 1 only)
 //   work   DP tree levels when the leaves must survive (k > 1 threshold scan)
 //   split  DP tree argmin (uint8 e of the left subtree), ~M * (R + 1) bytes
 struct Slice {
-    int64_t rows, cyc, cnt, st0, st1, G, H, work, split, total;
+    int64_t rows, cyc, cost, cnt, st0, st1, rng, G, H, work, split, total;
 };
 
 __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -71,9 +73,11 @@ __host__ __device__ inline Slice make_slice(int mmax, int r1max, int tab, int ta
     const int64_t tmax = tab > tab_kc ? tab : tab_kc;
     s.rows = o;  o = align16(o + int64_t(mmax) * kRows * 8);
     s.cyc = o;   o = align16(o + int64_t(mmax) * 4 * 8);
+    s.cost = o;  o = align16(o + int64_t(mmax) * 6 * 8);
     s.cnt = o;   o = align16(o + int64_t(mmax) * 4);
     s.st0 = o;   o = align16(o + int64_t(mmax) * 4);
     s.st1 = o;   o = align16(o + int64_t(mmax) * 4);
+    s.rng = o;   o = align16(o + int64_t(mmax) * 8);
     s.G = o;     o = align16(o + tmax * 8);
     s.H = o;     o = align16(o + int64_t(tab_kc) * 8);
     s.work = o;  o = align16(o + (tab_kc > 0 ? (int64_t(tab_kc) / 2 + 2 * int64_t(r1max) + 2) * 8 : 0));
@@ -149,8 +153,16 @@ __global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, hal
             infeas = wave_or(infeas);
             sumlo = wave_sum(sumlo);
             if (bad) status = HALDA_STATUS_UNSUPPORTED;
-            else if (infeas || sumlo > W) status = HALDA_STATUS_INFEASIBLE;
-            else {
+            else if (infeas || sumlo > W || (M == 0 && W > 0)) status = HALDA_STATUS_INFEASIBLE;
+            else if (M == 0) {  // no devices and W = 0: x = [C = 0] is optimal
+                if (lane == 0) {
+                    cls[inst] = CLS_DONE;
+                    Rz.x[co] = 0.0;
+                    Rz.status[inst] = HALDA_STATUS_OPTIMAL;
+                    Rz.obj_lin[inst] = Rz.dual_bound[inst] = Rz.gap[inst] = 0.0;
+                    Rz.nodes[inst] = 0;
+                }
+            } else {
                 const int R1 = W - sumlo + 1;
                 const bool kc = B.c[co + 7 * M] > 0.0;
                 if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
@@ -166,13 +178,15 @@ __global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, hal
 
 // ---------------------------------------------------------------- solve
 // One device's data in registers (lane = device). Rows are regrouped per
-// slack: slack j has up to two rows (a, b) with need = u w + v n + K; pure
-// (w, n) rows (link n <= w) are the two "f" rows: u w + v n <= K.
+// slack: all rows of slack j share (u, v) (validated at decode; this is what
+// keeps the cost L-natural convex), so they merge into one requirement
+// s_j >= u_j w + v_j n + K_j with K_j the largest; pure (w, n) rows (the link
+// n <= w) are the two "f" rows: u w + v n <= K.
 struct Dev {
     double cw, cn, cs0, cs1, cs2, cs3, r1w, r2w, rhs1, rhs2;
     int wlo, whi, nlo, nhi;
     int slo[4], shi[4];
-    int ua[4], va[4], Ka[4], ub[4], vb[4], Kb[4];
+    int us[4], vs[4], Ks[4];
     int uf[2], vf[2], Kf[2];
 };
 
@@ -183,9 +197,7 @@ __device__ inline bool least_slacks(const Dev &d, int w, int n, int s[4]) {
     bool ok = d.uf[0] * w + d.vf[0] * n <= d.Kf[0] && d.uf[1] * w + d.vf[1] * n <= d.Kf[1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int a = d.ua[j] * w + d.va[j] * n + d.Ka[j];
-        const int b = d.ub[j] * w + d.vb[j] * n + d.Kb[j];
-        s[j] = max(d.slo[j], max(a, b));
+        s[j] = max(d.slo[j], d.us[j] * w + d.vs[j] * n + d.Ks[j]);
         ok = ok && s[j] <= d.shi[j];
     }
     return ok;
@@ -231,11 +243,9 @@ __device__ inline void n_interval(const Dev &d, int w, int &nL, int &nU) {
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int ra = d.shi[j] - d.ua[j] * w - d.Ka[j], rb = d.shi[j] - d.ub[j] * w - d.Kb[j];  // v n <= r
-        if (d.va[j] > 0) nU = min(nU, ra);
-        if (d.va[j] < 0) nL = max(nL, -ra);
-        if (d.vb[j] > 0) nU = min(nU, rb);
-        if (d.vb[j] < 0) nL = max(nL, -rb);
+        const int r = d.shi[j] - d.us[j] * w - d.Ks[j];  // v n <= r
+        if (d.vs[j] > 0) nU = min(nU, r);
+        if (d.vs[j] < 0) nL = max(nL, -r);
     }
 }
 
@@ -266,10 +276,8 @@ __device__ inline bool split_full(const Dev &d, int w, double &g, int &n, int s[
     try_split(d, w, nL, nL, nU, best, bn, s);
     try_split(d, w, nU, nL, nU, best, bn, s);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (d.va[j] != 0) try_split(d, w, d.va[j] * (d.slo[j] - d.ua[j] * w - d.Ka[j]), nL, nU, best, bn, s);
-        if (d.vb[j] != 0) try_split(d, w, d.vb[j] * (d.slo[j] - d.ub[j] * w - d.Kb[j]), nL, nU, best, bn, s);
-    }
+    for (int j = 0; j < 4; ++j)
+        if (d.vs[j] != 0) try_split(d, w, d.vs[j] * (d.slo[j] - d.us[j] * w - d.Ks[j]), nL, nU, best, bn, s);
     if (bn < 0) return false;
     g = best;
     n = bn;
@@ -294,21 +302,21 @@ __device__ inline bool split_step(const Dev &d, int w, int n_prev, double &g, in
 }
 
 struct WaveCtx {
-    int2 *rows;
-    double *cyc;
+    int2 *rows;    // [i][q] packed capacity rows
+    double *cyc;   // [i] {r1w, r2w, rhs1, rhs2}
+    double *cost;  // [i] {cw, cn, cs0, cs1, cs2, cs3}
     int *cnt;
     int *st0, *st1;
+    int2 *rng;     // [slot] finite range of a DP-tree node (merge path)
     double *G, *H, *work;
     uint8_t *split;
 };
 
-__device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, int64_t co, int M, int i, double Wd) {
-    d.cw = B.c[co + i];
-    d.cn = B.c[co + M + i];
-    d.cs0 = B.c[co + 2 * M + i];
-    d.cs1 = B.c[co + 3 * M + i];
-    d.cs2 = B.c[co + 4 * M + i];
-    d.cs3 = B.c[co + 5 * M + i];
+// Device record: costs / decoded rows from LDS, integer bounds from the batch.
+__device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, int64_t co, int M, int i,
+                                double Wd) {
+    const double *c = w.cost + 6 * i;
+    d.cw = c[0]; d.cn = c[1]; d.cs0 = c[2]; d.cs1 = c[3]; d.cs2 = c[4]; d.cs3 = c[5];
     d.wlo = int(ceil(B.col_lb[co + i]));
     d.whi = int(floor(fmin(B.col_ub[co + i], Wd)));
     d.nlo = int(ceil(B.col_lb[co + M + i]));
@@ -317,18 +325,15 @@ __device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, 
     for (int j = 0; j < 4; ++j) {
         d.slo[j] = int(ceil(B.col_lb[co + (2 + j) * M + i]));
         d.shi[j] = int(floor(fmin(B.col_ub[co + (2 + j) * M + i], 1e6)));
-        d.ua[j] = d.va[j] = d.ub[j] = d.vb[j] = 0;
-        d.Ka[j] = d.Kb[j] = kNoRow;
+        d.us[j] = d.vs[j] = 0;
+        d.Ks[j] = kNoRow;
     }
     d.uf[0] = d.vf[0] = d.uf[1] = d.vf[1] = 0;
     d.Kf[0] = d.Kf[1] = 0;
-    d.r1w = w.cyc[4 * i + 0];
-    d.r2w = w.cyc[4 * i + 1];
-    d.rhs1 = w.cyc[4 * i + 2];
-    d.rhs2 = w.cyc[4 * i + 3];
+    const double *y = w.cyc + 4 * i;
+    d.r1w = y[0]; d.r2w = y[1]; d.rhs1 = y[2]; d.rhs2 = y[3];
     const int nrow = w.cnt[i] & 0xff;
     int nf = 0;
-    int seen[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < kRows; ++q) {
         if (q < nrow) {
@@ -342,13 +347,42 @@ __device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (kind == j) {
-                    if (seen[j] == 0) { d.ua[j] = u; d.va[j] = v; d.Ka[j] = r.y; }
-                    else { d.ub[j] = u; d.vb[j] = v; d.Kb[j] = r.y; }
-                    ++seen[j];
+                    d.us[j] = u;
+                    d.vs[j] = v;
+                    d.Ks[j] = max(d.Ks[j], r.y);
                 }
             }
         }
     }
+}
+
+// Leaf pre-pass of one DP call (lane = device): finite range [lo, hi] of the
+// leaf A_i[e] = G[i][e] (+inf where H[i][e] > T when use_T) into rng[i], and
+// whether the merge path applies: the finite set is an interval and A_i is
+// convex on it (increments non-decreasing up to 1e-12 relative). The cost is
+// L-natural convex in (w, n), so G_i (its minimum over n) is convex in w and its
+// threshold sublevel sets are intervals; the check guards the floating point.
+__device__ bool leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, int lane) {
+    bool ok = true;
+    for (int i = lane; i < M; i += 64) {
+        const double *G = w.G + int64_t(i) * RS, *H = w.H + int64_t(i) * RS;
+        int lo = R1, hi = -1, cnt = 0;
+        for (int e = 0; e < R1; ++e) {
+            const bool in = G[e] < kInf && (!use_T || H[e] <= T);
+            if (in) {
+                lo = min(lo, e);
+                hi = e;
+                ++cnt;
+            }
+        }
+        ok = ok && (cnt == 0 || cnt == hi - lo + 1);
+        for (int e = lo + 1; e < hi; ++e) {
+            const double d0 = G[e] - G[e - 1], d1 = G[e + 1] - G[e];
+            ok = ok && d1 >= d0 - 1e-12 * fmax(1.0, fabs(G[e]));
+        }
+        w.rng[i] = make_int2(lo, hi);
+    }
+    return !wave_or(!ok);
 }
 
 // Tree min-plus DP over the devices. Leaves: A_i[e] = G[i][e] (masked to +inf
@@ -357,7 +391,11 @@ __device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, 
 // an unpaired last node passes through. Output node p of level l lives in slot
 // p << (l - 1) of `buf` (in place over its left child; buf may be G itself when
 // the leaves are not needed again). Returns the root value at r = R (lane-uniform).
-__device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
+// convex: every node is a convex sequence on its finite range rng[slot], so
+// e -> L[e] + R[r - e] is convex and its least minimiser is found by binary
+// search on f(e + 1) >= f(e) (O(log R) per state); otherwise the O(R) scan.
+__device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane,
+                          bool convex) {
     if (M == 1) {
         const double g = w.G[R1 - 1];
         return (use_T && !(w.H[R1 - 1] <= T)) ? kInf : g;
@@ -370,11 +408,12 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
         const double *src = l == 1 ? w.G : buf;
         const int sh = l == 1 ? 0 : l - 2;  // slot shift of this level's inputs
         for (int p0 = 0; p0 < nout; p0 += npp) {
-            // each lane: one (node, r) task, or up to 4 states of one node when R1 > 64
-            double best[4] = {kInf, kInf, kInf, kInf};
-            int be[4] = {0, 0, 0, 0}, pp[4] = {-1, -1, -1, -1}, rr[4] = {0, 0, 0, 0};
+            // each lane: one (node, r) task, or two states of one node when R1 > 64
+            double best[2] = {kInf, kInf};
+            int be[2] = {0, 0}, pp[2] = {-1, -1}, rr[2] = {0, 0};
+            int2 orng[2] = {make_int2(0, -1), make_int2(0, -1)};
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < 2; ++t) {
                 int p, r;
                 if (R1 <= 64) {
                     const int k = lane / R1;
@@ -389,32 +428,68 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
                 pp[t] = p;
                 rr[t] = r;
                 const int a = 2 * p, b = 2 * p + 1;
-                const double *A = src + (int64_t(a) << sh) * RS;
+                const int sa = a << sh, sb = b << sh;
+                const double *A = src + int64_t(sa) * RS;
                 if (b < n) {
-                    const double *Bv = src + (int64_t(b) << sh) * RS;
-                    const double *HA = w.H + int64_t(a) * RS, *HB = w.H + int64_t(b) * RS;
-                    for (int e = 0; e <= r; ++e) {
-                        double x = A[e], y = Bv[r - e];
-                        if (l == 1 && use_T) {
-                            if (!(HA[e] <= T)) x = kInf;
-                            if (!(HB[r - e] <= T)) y = kInf;
+                    const double *Bv = src + int64_t(sb) * RS;
+                    if (convex) {
+                        const int2 ra = w.rng[sa], rb = w.rng[sb];
+                        orng[t] = make_int2(ra.x + rb.x, min(ra.y + rb.y, R1 - 1));
+                        int lo = max(ra.x, r - rb.y), hi = min(ra.y, r - rb.x);
+                        if (lo <= hi) {
+                            while (lo < hi) {
+                                const int mid = (lo + hi) >> 1;
+                                const double f0 = A[mid] + Bv[r - mid], f1 = A[mid + 1] + Bv[r - mid - 1];
+                                if (f1 >= f0) hi = mid;
+                                else lo = mid + 1;
+                            }
+                            best[t] = A[lo] + Bv[r - lo];
+                            be[t] = lo;
                         }
-                        const double v = x + y;
-                        if (v < best[t]) { best[t] = v; be[t] = e; }
+                    } else {
+                        const bool masked = l == 1 && use_T;
+                        const double *HA = w.H + int64_t(a) * RS, *HB = w.H + int64_t(b) * RS;
+                        // e runs to R1 - 1 on every lane in blocks of 8 (16 LDS reads in
+                        // flight before the first use); e > r is masked
+                        for (int e0 = 0; e0 < R1; e0 += 8) {
+                            double xs[8], ys[8];
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                const int ea = min(e0 + k, R1 - 1), eb = max(r - e0 - k, 0);
+                                xs[k] = A[ea];
+                                ys[k] = Bv[eb];
+                                if (masked) {
+                                    if (!(HA[ea] <= T)) xs[k] = kInf;
+                                    if (!(HB[eb] <= T)) ys[k] = kInf;
+                                }
+                            }
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                const double v = xs[k] + ys[k];
+                                if (e0 + k <= r && v < best[t]) { best[t] = v; be[t] = e0 + k; }
+                            }
+                        }
                     }
                 } else {
                     double x = A[r];
-                    if (l == 1 && use_T && !(w.H[int64_t(a) * RS + r] <= T)) x = kInf;
+                    if (convex) {
+                        orng[t] = w.rng[sa];
+                        if (r < orng[t].x || r > orng[t].y) x = kInf;
+                    } else if (l == 1 && use_T && !(w.H[int64_t(a) * RS + r] <= T)) {
+                        x = kInf;
+                    }
                     best[t] = x;
                     be[t] = r;
                 }
             }
             wave_sync();  // every read of this pass before any write
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < 2; ++t) {
                 if (pp[t] >= 0) {
-                    buf[(int64_t(pp[t]) << (l - 1)) * RS + rr[t]] = best[t];
+                    const int slot = pp[t] << (l - 1);
+                    buf[int64_t(slot) * RS + rr[t]] = best[t];
                     w.split[soff + pp[t] * R1 + rr[t]] = uint8_t(be[t]);
+                    if (convex && rr[t] == 0) w.rng[slot] = orng[t];
                 }
             }
             wave_sync();
@@ -423,6 +498,13 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
         n = nout;
     }
     return buf[R1 - 1];
+}
+
+// One DP call: leaf ranges / convexity check, then the tree.
+__device__ double dp_call(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
+    const bool convex = M > 1 && leaf_ranges(w, M, R1, RS, use_T, T, lane);
+    wave_sync();
+    return tree_dp(w, M, R1, RS, use_T, T, buf, lane, convex);
 }
 
 // Walk the tree top-down from the root state R: st0[i] = e_i of device i.
@@ -465,7 +547,338 @@ __device__ void tree_backtrack(const WaveCtx &w, int M, int R1, int lane) {
     }
 }
 
-__global__ __launch_bounds__(64) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
+struct Inst {
+    int inst, m, M, iC, W, R1, RS;
+    float invM;
+    int64_t co, ro;
+    const int32_t *rp;
+    double Wd, kc;
+};
+
+// Device pass (lane = device): cost / bound / integrality checks, and the
+// device's objective entries into LDS. Returns sum_i lb(w_i) on every lane
+// and ORs failures into bad.
+__device__ int device_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane, int &bad) {
+    const int M = I.M;
+    const int64_t co = I.co;
+    int sumlo = 0;
+    for (int i = lane; i < M; i += 64) {
+        double cv[6];
+        uint8_t ig[6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            cv[b] = B.c[co + b * M + i];
+            ig[b] = B.integrality[co + b * M + i];
+        }
+        const double lbw = B.col_lb[co + i], lbn = B.col_lb[co + M + i];
+        const double cz = B.c[co + 6 * M + i], lz = B.col_lb[co + 6 * M + i], uz = B.col_ub[co + 6 * M + i];
+        const uint8_t iz = B.integrality[co + 6 * M + i];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            bad |= ig[b] != 1;
+            w.cost[6 * i + b] = cv[b];
+        }
+        bad |= iz != 0 || cz != 0.0 || lz != 0.0 || uz != kInf || lbn < 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bad |= !(cv[2 + j] >= 0.0);
+        sumlo += int(ceil(lbw));
+        w.cnt[i] = 0;
+    }
+    if (lane == 0)
+        bad |= !(I.kc >= 0.0) || B.integrality[I.co + I.iC] != 0 || B.col_lb[I.co + I.iC] != 0.0 ||
+               B.col_ub[I.co + I.iC] != kInf;
+    return wave_sum(sumlo);
+}
+
+// j = blk * M + i with 0 <= i < M, without an integer division (j < 2^24).
+__device__ inline int block_of(int j, int M, float invM) {
+    int q = int(float(j) * invM);
+    q += (q + 1) * M <= j;
+    q -= q * M > j;
+    return q;
+}
+
+// Classify one CSR row by its nonzero pattern and record it for its device.
+// Returns nonzero when the row does not fit the HALDA structure.
+__device__ inline int decode_row(const WaveCtx &w, const Inst &I, int nnz, double rhs, double rlb,
+                                 const int (&cols)[kMaxRowNnz], const double (&vals)[kMaxRowNnz]) {
+    const int M = I.M;
+    if (rlb != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs) < 1e300)) return 1;
+    int last = -1, zc = -1;
+    double vlast = 0.0, vz = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxRowNnz; ++k) {
+        if (k == nnz - 1) { last = cols[k]; vlast = vals[k]; }
+        if (k == nnz - 2) { zc = cols[k]; vz = vals[k]; }
+    }
+    int rb = 0;
+    if (last == I.iC) {
+        // cycle row: busy(i) +- z_i - C <= rhs; its non-w part must equal the objective's
+        const int dev = zc - 6 * M;
+        if (vlast != -1.0 || nnz < 2 || dev < 0 || dev >= M || fabs(vz) != 1.0) return 1;
+        const double *cst = w.cost + 6 * dev;
+        double coef0 = 0.0;
+        int seen = 0;  // bitmask of blocks present
+#pragma unroll
+        for (int k = 0; k < kMaxRowNnz; ++k) {
+            if (k < nnz - 2) {
+                const int j = cols[k];
+                const int blk = block_of(j, M, I.invM);
+                if (j >= 6 * M || j - blk * M != dev) rb = 1;
+                else if (blk == 0) coef0 = vals[k];
+                else {
+                    rb |= vals[k] != cst[blk];
+                    seen |= 1 << blk;
+                }
+            }
+        }
+        // absent entries must be zero in the objective too
+#pragma unroll
+        for (int b = 1; b < 6; ++b) rb |= !((seen >> b) & 1) && cst[b] != 0.0;
+        if (!rb) {
+            const bool first = vz > 0.0;
+            w.cyc[4 * dev + (first ? 0 : 1)] = coef0;
+            w.cyc[4 * dev + (first ? 2 : 3)] = rhs;
+            atomicAdd(&w.cnt[dev], first ? (1 << 8) : (1 << 16));
+        }
+        return rb;
+    }
+    // capacity / link row of one device: aw w + an n - beta s <= rhs
+    int dev = -1, slack = -1;
+    double aw = 0.0, an = 0.0, beta = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxRowNnz; ++k) {
+        if (k < nnz) {
+            const int j = cols[k], blk = block_of(j, M, I.invM), i = j - blk * M;
+            if (j >= 6 * M || (dev >= 0 && i != dev)) rb = 1;
+            dev = i;
+            if (blk == 0) aw = vals[k];
+            else if (blk == 1) an = vals[k];
+            else if (slack >= 0) rb = 1;
+            else { slack = blk - 2; beta = -vals[k]; }
+        }
+    }
+    const double scale = slack >= 0 ? beta : fmax(fabs(aw), fabs(an));
+    rb |= !(scale > 0.0) || !(aw == 0.0 || fabs(aw) == scale) || !(an == 0.0 || fabs(an) == scale);
+    const int u = aw == 0.0 ? 0 : (aw > 0.0 ? 1 : -1);
+    const int v = an == 0.0 ? 0 : (an > 0.0 ? 1 : -1);
+    rb |= u * v > 0;  // L-natural convexity: w and n may be coupled only through w - n
+    if (rb) return 1;
+    const double kk = slack >= 0 ? ceil(-rhs / beta - kSlackEps)
+                                 : floor((rhs + kSlackEps * fmax(1.0, fabs(rhs))) / scale);
+    if (!(fabs(kk) < 1e8)) return 1;
+    const int q = atomicAdd(&w.cnt[dev], 1) & 0xff;
+    if (q >= kRows) return 1;
+    w.rows[dev * kRows + q] = make_int2((slack + 1) | ((u + 1) << 8) | ((v + 1) << 16), int(kk));
+    return 0;
+}
+
+// Row pass: lane-strided rows, two rows per lane per step; the next step's row
+// pointers / bounds are loaded together with this step's entries (one global
+// round trip per step).
+__device__ int row_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane) {
+    const int nr = I.m - 1;
+    int bad = 0;
+    int rs[2], re[2];
+    double rhs[2], rlb[2];
+    auto meta = [&](int r0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = r0 + 64 * h + lane;
+            const bool in = r < nr;
+            rs[h] = in ? I.rp[r] : 0;
+            re[h] = in ? I.rp[r + 1] : 0;
+            rhs[h] = in ? B.row_ub[I.ro + r] : 0.0;
+            rlb[h] = in ? B.row_lb[I.ro + r] : -kInf;
+        }
+    };
+    meta(0);
+    for (int r0 = 0; r0 < nr; r0 += 128) {
+        int cols[2][kMaxRowNnz];
+        double vals[2][kMaxRowNnz];
+        int nnz[2];
+        double hr[2], lr[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            nnz[h] = re[h] - rs[h];
+            hr[h] = rhs[h];
+            lr[h] = rlb[h];
+#pragma unroll
+            for (int k = 0; k < kMaxRowNnz; ++k) {
+                const bool in = k < nnz[h];
+                cols[h][k] = in ? B.col_idx[rs[h] + k] : -1;
+                vals[h][k] = in ? B.val[rs[h] + k] : 0.0;
+            }
+        }
+        if (r0 + 128 < nr) meta(r0 + 128);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (r0 + 64 * h + lane < nr) bad |= decode_row(w, I, nnz[h], hr[h], lr[h], cols[h], vals[h]);
+    }
+    return bad;
+}
+
+// Per device: one row of each cycle kind, <= 2 pure rows, and the rows of one
+// slack share their (u, v) pattern.
+__device__ int check_rows(const WaveCtx &w, int M, int lane) {
+    int bad = 0;
+    for (int i = lane; i < M; i += 64) {
+        const int c = w.cnt[i], nr = min(c & 0xff, kRows);
+        bad |= (c & 0xff) > kRows || ((c >> 8) & 0xff) != 1 || ((c >> 16) & 0xff) != 1;
+        int pure = 0;
+        for (int q = 0; q < nr; ++q) {
+            const int x = w.rows[i * kRows + q].x, kind = (x & 0xff) - 1;
+            pure += kind < 0;
+            for (int q2 = 0; q2 < q; ++q2) {
+                const int x2 = w.rows[i * kRows + q2].x;
+                bad |= kind >= 0 && (x2 & 0xff) == (x & 0xff) && (x2 >> 8) != (x >> 8);
+            }
+        }
+        bad |= pure > 2;
+    }
+    return bad;
+}
+
+// Table pass (lane = device): G[i][e] (and H[i][e] for k > 1), w = lb + e.
+__device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane) {
+    for (int i = lane; i < I.M; i += 64) {
+        Dev d;
+        load_dev(d, B, w, I.co, I.M, i, I.Wd);
+        int n = 0, s[4];
+        bool have = false;
+        for (int e = 0; e < I.R1; ++e) {
+            const int wl = d.wlo + e;
+            double g = kInf, h = kInf;
+            bool ok = false;
+            if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
+            if (ok && I.kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
+            have = ok;
+            w.G[i * I.RS + e] = ok ? g : kInf;
+            if (I.kc > 0.0) w.H[i * I.RS + e] = h;
+        }
+    }
+}
+
+// DP pass; k > 1: ascending threshold scan with bound pruning. One tree_dp call
+// site: phase 0 = unconstrained, 1 = threshold scan, 2 = final re-run. Leaves the
+// chosen e_i in st0; returns false when infeasible.
+__device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &nodes) {
+    const int M = I.M, R1 = I.R1, RS = I.RS;
+    const double kc = I.kc;
+    double *buf = kc > 0.0 ? w.work : w.G;
+    int phase = 0;
+    bool use_T = false;
+    double T = 0.0, s_inf = kInf, best = kInf, bestT = kInf, tprev = -1.0, tlo = 0.0;
+    nodes = 0;
+    while (true) {
+        const double st = dp_call(w, M, R1, RS, use_T, T, buf, lane);
+        ++nodes;
+        if (phase == 2) break;
+        if (phase == 0) {
+            s_inf = st;
+            if (!(st < kInf)) return false;
+            if (!(kc > 0.0)) break;  // k = 1: the splits of this pass are final
+            tree_backtrack(w, M, R1, lane);
+            double hmax = 0.0;
+            for (int i = lane; i < M; i += 64) {
+                hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
+                double mn = kInf;
+                for (int e = 0; e < R1; ++e)
+                    if (w.G[i * RS + e] < kInf) mn = fmin(mn, w.H[i * RS + e]);
+                tlo = fmax(tlo, mn);  // every assignment has max_i H_i >= max_i min_e H[i][e]
+            }
+            hmax = wave_max(hmax);
+            tlo = wave_max(tlo);
+            best = kc * hmax + s_inf;
+            phase = 1;
+        } else if (st < kInf && kc * T + st < best) {
+            best = kc * T + st;
+            bestT = T;
+        }
+        if (phase == 1) {
+            if (use_T) tprev = T;
+            double t = kInf;
+            for (int i = lane; i < M; i += 64)
+                for (int e = 0; e < R1; ++e) {
+                    const double h = w.H[i * RS + e];
+                    if (w.G[i * RS + e] < kInf && h >= tlo && h > tprev) t = fmin(t, h);
+                }
+            t = wave_min(t);
+            if (t < kInf && kc * t + s_inf < best) {
+                use_T = true;
+                T = t;
+                continue;
+            }
+            if (!use_T && !(bestT < kInf)) break;  // no scan pass ran: phase-0 splits are final
+            phase = 2;
+            use_T = bestT < kInf;
+            T = bestT;
+        }
+    }
+    tree_backtrack(w, M, R1, lane);
+    return true;
+}
+
+// Output pass (lane = device): x = (w, n, least slacks, stall z, cycle time C), obj_lin.
+__device__ void output_pass(const halda_batch &B, const halda_result &Rz, const WaveCtx &w, const Inst &I, int lane,
+                            int64_t nodes) {
+    const int M = I.M;
+    double hmax = 0.0;
+    double *x = Rz.x + I.co;
+    for (int i = lane; i < M; i += 64) {
+        Dev d;
+        load_dev(d, B, w, I.co, I.M, i, I.Wd);
+        const int wl = d.wlo + w.st0[i];
+        double g = 0.0, P, Q;
+        int n = 0, s[4] = {0, 0, 0, 0};
+        split_full(d, wl, g, n, s);
+        dev_cycle(d, wl, n, s, P, Q);
+        x[i] = double(wl);
+        x[M + i] = double(n);
+        x[2 * M + i] = double(s[0]);
+        x[3 * M + i] = double(s[1]);
+        x[4 * M + i] = double(s[2]);
+        x[5 * M + i] = double(s[3]);
+        x[6 * M + i] = Q > P ? 0.5 * (Q - P) : 0.0;
+        w.cyc[4 * i] = g;  // per-device cost scratch for the ordered sum below
+        hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
+    }
+    hmax = wave_max(hmax);
+    wave_sync();
+    if (lane == 0) {
+        double gsum = 0.0;
+        for (int i = 0; i < M; ++i) gsum = gsum + w.cyc[4 * i];
+        const double obj = gsum + I.kc * hmax;
+        x[I.iC] = hmax;
+        Rz.status[I.inst] = HALDA_STATUS_OPTIMAL;
+        Rz.obj_lin[I.inst] = obj;
+        Rz.dual_bound[I.inst] = obj;
+        Rz.gap[I.inst] = 0.0;
+        Rz.nodes[I.inst] = nodes;
+    }
+    wave_sync();
+}
+
+// Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
+// phase boundaries of the solve kernel, read back with halda_debug_stamps().
+#ifdef HALDA_STAMPS
+constexpr int kStampInst = 65536, kStamps = 8;
+__device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
+#define HALDA_STAMP(k)                                                                                  \
+    do {                                                                                                \
+        if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define HALDA_STAMP(k) \
+    do {               \
+    } while (0)
+#endif
+
+#ifndef HALDA_SOLVE_WAVES_PER_SIMD
+#define HALDA_SOLVE_WAVES_PER_SIMD 2  // occupancy target of the solve kernel (register budget)
+#endif
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
                                                           int mmax, int r1max, int tab, int tab_kc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -473,16 +886,18 @@ __global__ __launch_bounds__(64) void halda_solve_kernel(halda_batch B, halda_re
     WaveCtx w;
     w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
     w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
+    w.cost = reinterpret_cast<double *>(smem + sl.cost);
     w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
     w.st0 = reinterpret_cast<int *>(smem + sl.st0);
     w.st1 = reinterpret_cast<int *>(smem + sl.st1);
+    w.rng = reinterpret_cast<int2 *>(smem + sl.rng);
     w.G = reinterpret_cast<double *>(smem + sl.G);
     w.H = reinterpret_cast<double *>(smem + sl.H);
     w.work = reinterpret_cast<double *>(smem + sl.work);
     w.split = smem + sl.split;
 
     // this wave owns instances blockIdx.x + j * gridDim.x; a 64-wide window of
-    // them is screened by one ballot over cls
+    // them is screened by one ballot over the verdict bytes
     const int S = gridDim.x;
     for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
         const int64_t mine = base + int64_t(lane) * S;
@@ -491,273 +906,47 @@ __global__ __launch_bounds__(64) void halda_solve_kernel(halda_batch B, halda_re
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const int inst = int(base + int64_t(bit) * S);
+            Inst I;
+            I.inst = int(base + int64_t(bit) * S);
+            const int N = B.n_cols[I.inst];
+            I.m = B.n_rows[I.inst];
+            I.M = (N - 1) / 7;
+            I.iC = 7 * I.M;
+            I.invM = 1.0f / float(I.M);
+            I.co = B.col_off[I.inst];
+            I.ro = B.row_off[I.inst];
+            I.rp = B.row_ptr + B.csr_off[I.inst];
+            I.Wd = B.row_ub[I.ro + I.m - 1];
+            I.W = int(I.Wd);
+            I.kc = B.c[I.co + I.iC];
+            HALDA_STAMP(0);
 
-            const int N = B.n_cols[inst], m = B.n_rows[inst];
-            const int M = (N - 1) / 7, iC = 7 * M;
-            const int64_t co = B.col_off[inst], ro = B.row_off[inst];
-            const int32_t *rp = B.row_ptr + B.csr_off[inst];
-            const double Wd = B.row_ub[ro + m - 1];
-            const int W = int(Wd);
-            const double kc = B.c[co + iC];
-
-            // ---- per-device checks on costs / bounds / integrality; reset row slots
-            int bad = 0, sumlo = 0;
-            for (int i = lane; i < M; i += 64) {
-                for (int b = 0; b < 6; ++b) bad |= B.integrality[co + b * M + i] != 1;
-                bad |= B.integrality[co + 6 * M + i] != 0 || B.c[co + 6 * M + i] != 0.0;
-                bad |= B.col_lb[co + 6 * M + i] != 0.0 || B.col_ub[co + 6 * M + i] != kInf;
-                bad |= B.col_lb[co + M + i] < 0.0;
-                for (int j = 0; j < 4; ++j) bad |= !(B.c[co + (2 + j) * M + i] >= 0.0);
-                sumlo += int(ceil(B.col_lb[co + i]));
-                w.cnt[i] = 0;
-            }
-            if (lane == 0)
-                bad |= !(kc >= 0.0) || B.integrality[co + iC] != 0 || B.col_lb[co + iC] != 0.0 ||
-                       B.col_ub[co + iC] != kInf;
-            sumlo = wave_sum(sumlo);
-            const int R1 = W - sumlo + 1, RS = odd_stride(R1);
+            int bad = 0;
+            const int sumlo = device_pass(B, w, I, lane, bad);
+            I.R1 = I.W - sumlo + 1;
+            I.RS = odd_stride(I.R1);
             wave_sync();
-
-            // ---- rows: classify by nonzero pattern (lane-strided, two rows per lane in flight)
-            for (int r0 = 0; r0 < m - 1; r0 += 128) {
-                int rs[2], re[2];
-                double rhs[2], rlb[2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int r = r0 + 64 * h + lane;
-                    const bool in = r < m - 1;
-                    rs[h] = in ? rp[r] : 0;
-                    re[h] = in ? rp[r + 1] : 0;
-                    rhs[h] = in ? B.row_ub[ro + r] : 0.0;
-                    rlb[h] = in ? B.row_lb[ro + r] : -kInf;
-                }
-                int cols[2][kMaxRowNnz];
-                double vals[2][kMaxRowNnz];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int nnz = re[h] - rs[h];
-#pragma unroll
-                    for (int k = 0; k < kMaxRowNnz; ++k) {
-                        const bool in = k < nnz;
-                        cols[h][k] = in ? B.col_idx[rs[h] + k] : -1;
-                        vals[h][k] = in ? B.val[rs[h] + k] : 0.0;
-                    }
-                }
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int r = r0 + 64 * h + lane;
-                    if (r >= m - 1) continue;
-                    const int nnz = re[h] - rs[h];
-                    int rb = rlb[h] != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs[h]) < 1e300);
-                    if (rb) { bad = 1; continue; }
-                    int last = -1, zc = -1;
-                    double vlast = 0.0, vz = 0.0;
-#pragma unroll
-                    for (int k = 0; k < kMaxRowNnz; ++k) {
-                        if (k == nnz - 1) { last = cols[h][k]; vlast = vals[h][k]; }
-                        if (k == nnz - 2) { zc = cols[h][k]; vz = vals[h][k]; }
-                    }
-                    if (last == iC) {
-                        // cycle row: busy(i) +- z_i - C <= rhs; its non-w part must equal the objective's
-                        const int dev = zc - 6 * M;
-                        rb |= vlast != -1.0 || nnz < 2 || dev < 0 || dev >= M || fabs(vz) != 1.0;
-                        double coef[6] = {0, 0, 0, 0, 0, 0};
-                        if (!rb) {
-#pragma unroll
-                            for (int k = 0; k < kMaxRowNnz; ++k) {
-                                if (k < nnz - 2) {
-                                    const int j = cols[h][k];
-                                    if (j >= 6 * M || j % M != dev) rb = 1;
-                                    else {
-                                        const int blk = j / M;
-#pragma unroll
-                                        for (int b = 0; b < 6; ++b)
-                                            if (blk == b) coef[b] = vals[h][k];
-                                    }
-                                }
-                            }
-                        }
-                        if (!rb) {
-#pragma unroll
-                            for (int b = 1; b < 6; ++b) rb |= coef[b] != B.c[co + b * M + dev];
-                        }
-                        if (!rb) {
-                            const bool first = vz > 0.0;
-                            w.cyc[4 * dev + (first ? 0 : 1)] = coef[0];
-                            w.cyc[4 * dev + (first ? 2 : 3)] = rhs[h];
-                            atomicAdd(&w.cnt[dev], first ? (1 << 8) : (1 << 16));
-                        }
-                    } else {
-                        // capacity / link row of one device: aw w + an n - beta s <= rhs
-                        int dev = -1, slack = -1;
-                        double aw = 0.0, an = 0.0, beta = 0.0;
-#pragma unroll
-                        for (int k = 0; k < kMaxRowNnz; ++k) {
-                            if (k < nnz) {
-                                const int j = cols[h][k], blk = j / M, i = j % M;
-                                if (j >= 6 * M || (dev >= 0 && i != dev)) rb = 1;
-                                dev = i;
-                                if (blk == 0) aw = vals[h][k];
-                                else if (blk == 1) an = vals[h][k];
-                                else if (slack >= 0) rb = 1;
-                                else { slack = blk - 2; beta = -vals[h][k]; }
-                            }
-                        }
-                        const double scale = slack >= 0 ? beta : fmax(fabs(aw), fabs(an));
-                        rb |= !(scale > 0.0) || !(aw == 0.0 || fabs(aw) == scale) ||
-                              !(an == 0.0 || fabs(an) == scale);
-                        const int u = aw == 0.0 ? 0 : (aw > 0.0 ? 1 : -1);
-                        const int v = an == 0.0 ? 0 : (an > 0.0 ? 1 : -1);
-                        // L-natural convexity: a row may couple w and n only through w - n
-                        rb |= u * v > 0;
-                        if (!rb) {
-                            const double kk = slack >= 0
-                                                  ? ceil(-rhs[h] / beta - kSlackEps)
-                                                  : floor((rhs[h] + kSlackEps * fmax(1.0, fabs(rhs[h]))) / scale);
-                            rb |= !(fabs(kk) < 1e8);
-                            if (!rb) {
-                                const int q = atomicAdd(&w.cnt[dev], 1) & 0xff;
-                                if (q >= kRows) rb = 1;
-                                else
-                                    w.rows[dev * kRows + q] =
-                                        make_int2((slack + 1) | ((u + 1) << 8) | ((v + 1) << 16), int(kk));
-                            }
-                        }
-                    }
-                    bad |= rb;
-                }
-            }
+            HALDA_STAMP(1);
+            bad |= row_pass(B, w, I, lane);
             wave_sync();
-            // every device: one row of each cycle kind, <= 2 rows per slack, <= 2 pure rows
-            for (int i = lane; i < M; i += 64) {
-                const int c = w.cnt[i], nr = min(c & 0xff, kRows);
-                bad |= (c & 0xff) > kRows || ((c >> 8) & 0xff) != 1 || ((c >> 16) & 0xff) != 1;
-                int per[5] = {0, 0, 0, 0, 0};
-                for (int q = 0; q < nr; ++q) {
-                    const int kind = (w.rows[i * kRows + q].x & 0xff) - 1;
-                    for (int j = 0; j < 5; ++j) per[j] += (kind == j - 1);
-                }
-                for (int j = 0; j < 5; ++j) bad |= per[j] > 2;
-            }
-            bad = wave_or(bad);
-            if (bad) {
-                if (lane == 0) write_done(Rz, inst, HALDA_STATUS_UNSUPPORTED, 0);
+            HALDA_STAMP(2);
+            bad |= check_rows(w, I.M, lane);
+            if (wave_or(bad)) {
+                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
                 continue;
             }
-
-            // ---- tables: lane = device, e = 0..R: G[i][e], H[i][e]
-            for (int i = lane; i < M; i += 64) {
-                Dev d;
-                load_dev(d, B, w, co, M, i, Wd);
-                int n = 0, s[4];
-                bool have = false;
-                for (int e = 0; e < R1; ++e) {
-                    const int wl = d.wlo + e;
-                    double g = kInf, h = kInf;
-                    bool ok = false;
-                    if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
-                    if (ok && kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
-                    have = ok;
-                    w.G[i * RS + e] = ok ? g : kInf;
-                    if (kc > 0.0) w.H[i * RS + e] = h;
-                }
-            }
+            HALDA_STAMP(3);
+            table_pass(B, w, I, lane);
             wave_sync();
-
-            // ---- DP; k > 1: ascending threshold scan with bound pruning. One call
-            // site: phase 0 = unconstrained, 1 = threshold scan, 2 = final re-run.
-            double *buf = kc > 0.0 ? w.work : w.G;
+            HALDA_STAMP(4);
             int64_t nodes = 0;
-            int phase = 0;
-            bool use_T = false, feasible = true;
-            double T = 0.0, s_inf = kInf, best = kInf, bestT = kInf, tprev = -1.0, tlo = 0.0;
-            while (true) {
-                const double st = tree_dp(w, M, R1, RS, use_T, T, buf, lane);
-                ++nodes;
-                if (phase == 2) break;
-                if (phase == 0) {
-                    s_inf = st;
-                    if (!(st < kInf)) { feasible = false; break; }
-                    if (!(kc > 0.0)) break;  // k = 1: the splits of this pass are final
-                    tree_backtrack(w, M, R1, lane);
-                    double hmax = 0.0;
-                    for (int i = lane; i < M; i += 64) {
-                        hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
-                        double mn = kInf;
-                        for (int e = 0; e < R1; ++e)
-                            if (w.G[i * RS + e] < kInf) mn = fmin(mn, w.H[i * RS + e]);
-                        tlo = fmax(tlo, mn);  // every assignment has max_i H_i >= max_i min_e H[i][e]
-                    }
-                    hmax = wave_max(hmax);
-                    tlo = wave_max(tlo);
-                    best = kc * hmax + s_inf;
-                    phase = 1;
-                } else if (st < kInf && kc * T + st < best) {
-                    best = kc * T + st;
-                    bestT = T;
-                }
-                if (phase == 1) {
-                    if (use_T) tprev = T;
-                    double t = kInf;
-                    for (int i = lane; i < M; i += 64)
-                        for (int e = 0; e < R1; ++e) {
-                            const double h = w.H[i * RS + e];
-                            if (w.G[i * RS + e] < kInf && h >= tlo && h > tprev) t = fmin(t, h);
-                        }
-                    t = wave_min(t);
-                    if (t < kInf && kc * t + s_inf < best) {
-                        use_T = true;
-                        T = t;
-                        continue;
-                    }
-                    if (!use_T && !(bestT < kInf)) break;  // no scan pass ran: phase-0 splits are final
-                    phase = 2;
-                    use_T = bestT < kInf;
-                    T = bestT;
-                }
-            }
-            if (!feasible) {
-                if (lane == 0) write_done(Rz, inst, HALDA_STATUS_INFEASIBLE, nodes);
+            if (!dp_pass(w, I, lane, nodes)) {
+                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_INFEASIBLE, nodes);
                 continue;
             }
-            tree_backtrack(w, M, R1, lane);
-
-            // ---- rebuild x for the chosen w: n, least slacks, stall z, cycle time C
-            double hmax = 0.0;
-            for (int i = lane; i < M; i += 64) {
-                Dev d;
-                load_dev(d, B, w, co, M, i, Wd);
-                const int wl = d.wlo + w.st0[i];
-                double g = 0.0, P, Q;
-                int n = 0, s[4] = {0, 0, 0, 0};
-                split_full(d, wl, g, n, s);
-                dev_cycle(d, wl, n, s, P, Q);
-                double *x = Rz.x + co;
-                x[i] = double(wl);
-                x[M + i] = double(n);
-                x[2 * M + i] = double(s[0]);
-                x[3 * M + i] = double(s[1]);
-                x[4 * M + i] = double(s[2]);
-                x[5 * M + i] = double(s[3]);
-                x[6 * M + i] = Q > P ? 0.5 * (Q - P) : 0.0;
-                w.cyc[4 * i] = g;  // per-device cost scratch for the ordered sum below
-                hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
-            }
-            hmax = wave_max(hmax);
-            wave_sync();
-            if (lane == 0) {
-                double gsum = 0.0;
-                for (int i = 0; i < M; ++i) gsum = gsum + w.cyc[4 * i];
-                const double obj = gsum + kc * hmax;
-                Rz.x[co + iC] = hmax;
-                Rz.status[inst] = HALDA_STATUS_OPTIMAL;
-                Rz.obj_lin[inst] = obj;
-                Rz.dual_bound[inst] = obj;
-                Rz.gap[inst] = 0.0;
-                Rz.nodes[inst] = nodes;
-            }
-            wave_sync();
+            HALDA_STAMP(5);
+            output_pass(B, Rz, w, I, lane, nodes);
+            HALDA_STAMP(6);
         }
     }
 }
@@ -796,7 +985,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     if (in.n_inst <= 0) return HALDA_OK;
     if (in.max_cols < 1 || in.max_R1 < 1 || in.max_tab < 0 || in.max_tab_kc < 0)
         return fail(HALDA_E_ARG, "halda_batch shape summary (max_cols/max_R1/max_tab/max_tab_kc) not set");
-    if (in.max_R1 > 256) return fail(HALDA_E_ARG, "max_R1 > 256 (W - sum lb(w) must be < 256)");
+    if (in.max_R1 > 128) return fail(HALDA_E_ARG, "max_R1 > 128 (W - sum lb(w) must be < 128)");
     const int mmax = (in.max_cols - 1) / 7 + 1;
     // table sizes in doubles with the odd row stride used on chip
     // M * RS <= M * (R + 1) + M: the odd row stride costs at most one double per device
@@ -847,7 +1036,7 @@ int halda_last_error(char *buf, size_t len) {
 }
 
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc) {
-    if (max_R1 < 1 || max_R1 > 256) return -1;
+    if (max_R1 < 1 || max_R1 > 128) return -1;
     const int mmax = (max_cols - 1) / 7 + 1;
     const int64_t tab = std::max<int64_t>(1, max_tab > 0 ? int64_t(max_tab) + mmax : 0);
     const int64_t tab_kc = max_tab_kc > 0 ? int64_t(max_tab_kc) + mmax : 0;
@@ -921,6 +1110,15 @@ int halda_last_solve_kernel_ms(void *ctx, double *ms) {
     *ms = f;
     return HALDA_OK;
 }
+
+#ifdef HALDA_STAMPS
+int halda_debug_stamps(unsigned long long *out, int n_inst) {
+    const int n = std::min(n_inst, kStampInst);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halda_stamps), sizeof(unsigned long long) * kStamps * n));
+    return n;
+}
+#endif
 
 int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
     Ctx *c = static_cast<Ctx *>(ctx);

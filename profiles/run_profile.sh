@@ -14,3 +14,6 @@ timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format c
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_write" -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+# FETCH_SIZE calibration for 8-B and 16-B per-lane coalesced reads of a known byte count
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/calib" -o run -- \
+    ./build/hbm_calib > "$OUT/calib.json" 2> "$OUT/calib.err"

@@ -1,0 +1,62 @@
+"""Summarise a profiles/run_profile.sh run into profiles/<round>_*.
+
+Writes:
+  profiles/<R>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<R>_pmc.json           per-launch FETCH_SIZE / WRITE_SIZE of halda_solve_kernel and
+                                  halda_screen_kernel, the 8-B/lane FETCH_SIZE calibration and the
+                                  corrected HBM bytes per launch (read by bench.py as roofline.traffic)
+"""
+
+import csv
+import json
+import shutil
+import statistics
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def per_kernel(csv_path, counter):
+    vals = defaultdict(list)
+    for r in csv.DictReader(open(csv_path)):
+        if r["Counter_Name"] == counter:
+            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main(R):
+    src = REPO / "gpurun_out" / f"prof_{R}"
+    dst = REPO / "profiles"
+    shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{R}_kernel_stats.csv")
+    fetch = per_kernel(src / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
+    write = per_kernel(src / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
+    cal = per_kernel(src / "calib" / "run_counter_collection.csv", "FETCH_SIZE")
+    calib_bytes = 1 << 30
+    def pick(prefix):
+        return statistics.median(next(v for k, v in cal.items() if k.startswith(prefix))) * 1024 / calib_bytes
+
+    f8, f16 = pick("read8"), pick("read16")
+    out = {"fetch_size_over_bytes_8B_per_lane": f8, "fetch_size_over_bytes_16B_per_lane": f16, "kernels": {}}
+    for name in fetch:
+        if "halda" not in name:
+            continue
+        # the big C3 launches only (the bench also runs small time-to-optimal batches)
+        fk = max(fetch[name])
+        wk = max(write.get(name, [0.0]))
+        out["kernels"][name] = {
+            "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
+            "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
+        }
+    solve = out["kernels"].get("halda_solve_kernel")
+    out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
+    out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
+                   "coalesced read (tools/hbm_calib.hip), the solve kernel's dominant access width; "
+                   "WRITE_SIZE taken as bytes. Largest launch per kernel = the C3 batch.")
+    (dst / f"{R}_pmc.json").write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
