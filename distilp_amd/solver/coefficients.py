@@ -85,9 +85,12 @@ def gpu_load_throughput(dev: DeviceProfile) -> Optional[float]:
     return None
 
 
-def alpha_beta_xi(dev: DeviceProfile, model: ModelProfile, kv_factor: float = 1.0) -> Tuple[float, float, float]:
-    """(alpha, beta, xi): CPU s/layer, GPU-minus-CPU s/layer, fixed transfer s."""
-    bp = b_prime(model, kv_bits_k=kv_factor)
+def alpha_beta_xi(dev: DeviceProfile, model: ModelProfile, kv_factor: float = 1.0,
+                  bp: Optional[int] = None) -> Tuple[float, float, float]:
+    """(alpha, beta, xi): CPU s/layer, GPU-minus-CPU s/layer, fixed transfer s.
+    `bp` = b_prime(model, kv_factor) when the caller already has it."""
+    if bp is None:
+        bp = b_prime(model, kv_bits_k=kv_factor)
     cpu_comp = sum_f_over_s(model.f_q, dev.scpu, model.Q)
     alpha = cpu_comp + dev.t_kvcpy_cpu + (bp / dev.T_cpu)
     table, t_gpu = gpu_flops_table(dev), gpu_load_throughput(dev)
@@ -120,11 +123,12 @@ def objective_vectors(devs: List[DeviceProfile], model: ModelProfile, sets: Dict
                       kv_factor: float = 1.0) -> Tuple[List[float], List[float], List[float]]:
     """a = alpha, b = beta (0 for M1 devices), c = xi."""
     m1 = set(sets["M1"])
+    bp = b_prime(model, kv_bits_k=kv_factor)
     a: List[float] = []
     b: List[float] = []
     c: List[float] = []
     for i, d in enumerate(devs):
-        alpha, beta, xi = alpha_beta_xi(d, model, kv_factor)
+        alpha, beta, xi = alpha_beta_xi(d, model, kv_factor, bp)
         a.append(alpha)
         b.append(0.0 if i in m1 else beta)
         c.append(xi)

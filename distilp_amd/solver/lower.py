@@ -29,13 +29,22 @@ assembly itself is vectorised NumPy.
 
 from __future__ import annotations
 
+import operator
 from dataclasses import dataclass, field
 from typing import Dict, List, Sequence
 
 import numpy as np
 
 from ..common import DeviceProfile, ModelProfile
-from .coefficients import assign_sets, b_cio_b, b_prime, kappa_constant, objective_vectors
+from .coefficients import (
+    assign_sets,
+    b_prime,
+    gpu_flops_table,
+    gpu_load_throughput,
+    kappa_constant,
+    objective_vectors,
+    sum_f_over_s,
+)
 
 # variable blocks
 VAR_W, VAR_N, VAR_S1, VAR_S2, VAR_S3, VAR_T, VAR_Z = range(7)
@@ -72,23 +81,31 @@ class FleetMILP:
     def nnz(self) -> int:
         return int(self.val.shape[0])
 
+    def _bound_templates(self):
+        t = getattr(self, "_tpl", None)
+        if t is None:
+            M = self.M
+            lb = np.zeros(self.n_cols)
+            lb[:M] = 1.0
+            scale = np.zeros(self.n_cols)  # ub = W * scale on the integer columns
+            scale[:M] = 1.0
+            scale[M:2 * M] = self.gpu
+            for s in range(3):
+                scale[(2 + s) * M:(3 + s) * M] = self.in_set[s]
+            scale[5 * M:6 * M] = self.gpu
+            integ = np.ones(self.n_cols, dtype=np.uint8)
+            integ[6 * M:] = 0
+            t = self._tpl = (lb, scale, integ)
+        return t
+
     def col_bounds(self, W: int):
-        M = self.M
-        lb = np.zeros(self.n_cols)
-        ub = np.zeros(self.n_cols)
-        lb[:M] = 1.0
-        ub[:M] = W
-        ub[M:2 * M] = np.where(self.gpu, W, 0)
-        for s in range(3):
-            ub[(2 + s) * M:(3 + s) * M] = np.where(self.in_set[s], W, 0)
-        ub[5 * M:6 * M] = np.where(self.gpu, W, 0)
-        ub[6 * M:] = np.inf
-        return lb, ub
+        lb, scale, _ = self._bound_templates()
+        ub = scale * W
+        ub[6 * self.M:] = np.inf
+        return lb.copy(), ub
 
     def integrality(self) -> np.ndarray:
-        integ = np.ones(self.n_cols, dtype=np.uint8)
-        integ[6 * self.M:] = 0
-        return integ
+        return self._bound_templates()[2].copy()
 
     def instance(self, k: int):
         """(c, col_lb, col_ub, row_lb, row_ub, integrality, W) for one k."""
@@ -116,8 +133,84 @@ class FleetMILP:
         return A
 
 
+_FIELD_NAMES = ("Tc", "tkc", "tkg", "r2v", "v2r", "uma", "tcomm", "sdisk", "ram", "ccpu", "cgpu", "head", "has_cuda",
+                "cuda", "has_metal", "metal")
+_FIELDS = operator.attrgetter("T_cpu", "t_kvcpy_cpu", "t_kvcpy_gpu", "t_ram2vram", "t_vram2ram", "is_unified_mem",
+                              "t_comm", "s_disk", "d_avail_ram", "c_cpu", "c_gpu", "is_head", "has_cuda",
+                              "d_avail_cuda", "has_metal", "d_avail_metal")
+
+
+def _device_arrays(devs: Sequence[DeviceProfile], model: ModelProfile, sets, kv_factor: float):
+    """Per-device coefficients as NumPy arrays, element-wise in the reference's
+    operation order (dense_common.py:100-126, halda_p_solver.py:195-224), so every
+    value is bit-identical to the scalar restatement in coefficients.py.
+
+    Returns None when a device would make the reference raise (T_cpu == 0): the
+    caller then runs the scalar path, which raises the same exception."""
+    bp = b_prime(model, kv_bits_k=kv_factor)
+    Q = model.Q
+    cpu, gpu, has_beta, tg, swap = [], [], [], [], []
+    for d in devs:
+        c = sum_f_over_s(model.f_q, d.scpu, Q)  # raises ValueError like the reference
+        table, t_gpu = gpu_flops_table(d), gpu_load_throughput(d)
+        hb = table is not None and t_gpu is not None
+        cpu.append(c)
+        gpu.append(sum_f_over_s(model.f_q, table, Q) if hb else 0.0)
+        has_beta.append(hb)
+        tg.append(float(t_gpu) if hb else 1.0)
+        swap.append(min(d.d_bytes_can_swap, d.d_swap_avail) if d.os_type == "android" else 0)
+    cols = list(zip(*map(_FIELDS, devs))) if devs else [[] for _ in _FIELD_NAMES]
+    f = dict(zip(_FIELD_NAMES, cols))
+    f["swap"] = swap
+    f["cuda_ok"] = [bool(h and v is not None) for h, v in zip(f["has_cuda"], f["cuda"])]
+    f["metal_ok"] = [bool(h and v is not None) for h, v in zip(f["has_metal"], f["metal"])]
+    f["cuda"] = [0 if v is None else v for v in f["cuda"]]
+    f["metal"] = [0 if v is None else v for v in f["metal"]]
+    Tc = np.asarray(f["Tc"], dtype=np.float64)
+    if not np.all(Tc != 0.0):
+        return None
+    M = len(devs)
+    cpu = np.asarray(cpu, dtype=np.float64)
+    gpu = np.asarray(gpu, dtype=np.float64)
+    hb = np.asarray(has_beta, dtype=bool)
+    tg = np.asarray(tg, dtype=np.float64)
+    tkc = np.asarray(f["tkc"], dtype=np.float64)
+    tkg = np.asarray(f["tkg"], dtype=np.float64)
+    alpha = (cpu + tkc) + (bp / Tc)
+    beta = np.where(hb, ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc), 0.0)
+    m1 = np.zeros(M, dtype=bool)
+    m1[sets["M1"]] = True
+    m2 = np.zeros(M, dtype=bool)
+    m2[sets["M2"]] = True
+    b = np.where(m1, 0.0, beta)
+    xi = (np.asarray(f["r2v"], dtype=np.float64) + np.asarray(f["v2r"], dtype=np.float64)) * np.where(
+        np.asarray(f["uma"], dtype=bool), 0.0, 1.0)
+    head = np.where(np.asarray(f["head"], dtype=bool), 1.0, 0.0)
+    bcio = ((model.b_in / model.V) + model.b_out) * head + np.asarray(f["ccpu"], dtype=np.int64)
+    sd = np.maximum(1.0, np.asarray(f["sdisk"], dtype=np.float64))
+    pen_bp = bp / sd
+    pen_b = model.b_layer / sd
+    pen_v = np.where(m2, pen_b, pen_bp)
+    const = xi + np.asarray(f["tcomm"], dtype=np.float64)
+    S = np.stack([alpha, b, pen_bp, pen_b, pen_bp, pen_v, pen_bp, const], axis=1)
+    ram = np.asarray(f["ram"], dtype=np.int64)
+    cgpu = np.asarray(f["cgpu"], dtype=np.int64).astype(np.float64)
+    metal = np.asarray(f["metal"], dtype=np.int64).astype(np.float64)
+    rhs = {
+        "M1": ram.astype(np.float64) - bcio,
+        "M2": metal - bcio - cgpu,
+        "M3": (ram + np.asarray(f["swap"], dtype=np.int64)).astype(np.float64) - bcio,
+        "cuda": np.asarray(f["cuda"], dtype=np.int64).astype(np.float64) - cgpu,
+        "metal": metal - cgpu - float(model.b_out) * head,
+        "cuda_ok": np.asarray(f["cuda_ok"], dtype=bool),
+        "metal_ok": np.asarray(f["metal_ok"], dtype=bool),
+        "tcomm": f["tcomm"],
+    }
+    return bp, xi, S, rhs
+
+
 def _device_scalars(devs: Sequence[DeviceProfile], model: ModelProfile, sets, kv_factor: float):
-    """Per-device scalars in reference arithmetic (float ops kept in order)."""
+    """Scalar restatement (raises the reference's exceptions on degenerate inputs)."""
     bp = b_prime(model, kv_bits_k=kv_factor)
     a, b, xi = objective_vectors(list(devs), model, sets, kv_factor)
     m2 = set(sets["M2"])
@@ -142,7 +235,11 @@ def lower_fleet(devs: Sequence[DeviceProfile], model: ModelProfile, kv_bits: str
     if sets is None:
         sets = assign_sets(devs)
     kappa = kappa_constant(devs, model, sets)  # IndexError on an empty fleet, like the reference
-    bp, a, b, xi, S = _device_scalars(devs, model, sets, kv_factor)
+    arrays = _device_arrays(devs, model, sets, kv_factor)
+    if arrays is None:  # degenerate device: the scalar path raises like the reference
+        _device_scalars(devs, model, sets, kv_factor)
+        raise AssertionError("unreachable: degenerate device did not raise")
+    bp, xi, S, R = arrays
     bpf = float(bp)
     N = 7 * M + 1
     iC = 7 * M
@@ -157,43 +254,23 @@ def lower_fleet(devs: Sequence[DeviceProfile], model: ModelProfile, kv_bits: str
                        np.asarray(rhs, dtype=np.float64)))
 
     add(np.stack([idx, M + idx], 1), np.tile([-1.0, 1.0], (M, 1)), np.zeros(M))
-
-    def bcio(i):
-        return float(b_cio_b(devs[i], model))
-
-    m1 = sets["M1"]
-    if m1:
-        ii = np.asarray(m1)
-        add(np.stack([ii, 2 * M + ii], 1), np.tile([bpf, -bpf], (len(m1), 1)),
-            [float(devs[i].d_avail_ram) - bcio(i) for i in m1])
-    m2 = [i for i in sets["M2"] if devs[i].d_avail_metal is not None]
-    if m2:
-        ii = np.asarray(m2)
-        add(np.stack([ii, 3 * M + ii], 1), np.tile([bpf, -bpf], (len(m2), 1)),
-            [float(devs[i].d_avail_metal) - bcio(i) - float(devs[i].c_gpu) for i in m2])
-    m3 = sets["M3"]
-    if m3:
-        ii = np.asarray(m3)
-
-        def m3_rhs(i):
-            d = devs[i]
-            swap = min(d.d_bytes_can_swap, d.d_swap_avail) if d.os_type == "android" else 0
-            return float(d.d_avail_ram + swap) - bcio(i)
-
-        add(np.stack([ii, M + ii, 4 * M + ii], 1), np.tile([bpf, -bpf, -bpf], (len(m3), 1)),
-            [m3_rhs(i) for i in m3])
-    vram_dev, vram_rhs = [], []
-    for i, d in enumerate(devs):
-        if d.has_cuda and d.d_avail_cuda is not None:
-            vram_dev.append(i)
-            vram_rhs.append(float(d.d_avail_cuda) - float(d.c_gpu))
-        if d.has_metal and d.d_avail_metal is not None:
-            head = 1.0 if d.is_head else 0.0
-            vram_dev.append(i)
-            vram_rhs.append(float(d.d_avail_metal) - float(d.c_gpu) - float(model.b_out * head))
-    if vram_dev:
-        ii = np.asarray(vram_dev)
-        add(np.stack([M + ii, 5 * M + ii], 1), np.tile([bpf, -bpf], (len(ii), 1)), vram_rhs)
+    m1 = np.asarray(sets["M1"], dtype=np.int64)
+    if len(m1):
+        add(np.stack([m1, 2 * M + m1], 1), np.tile([bpf, -bpf], (len(m1), 1)), R["M1"][m1])
+    m2 = np.asarray([i for i in sets["M2"] if devs[i].d_avail_metal is not None], dtype=np.int64)
+    if len(m2):
+        add(np.stack([m2, 3 * M + m2], 1), np.tile([bpf, -bpf], (len(m2), 1)), R["M2"][m2])
+    m3 = np.asarray(sets["M3"], dtype=np.int64)
+    if len(m3):
+        add(np.stack([m3, M + m3, 4 * M + m3], 1), np.tile([bpf, -bpf, -bpf], (len(m3), 1)), R["M3"][m3])
+    # VRAM rows: per device the cuda row, then the metal row
+    vr_dev = np.concatenate([idx[R["cuda_ok"]], idx[R["metal_ok"]]])
+    vr_rhs = np.concatenate([R["cuda"][R["cuda_ok"]], R["metal"][R["metal_ok"]]])
+    vr_key = np.concatenate([2 * idx[R["cuda_ok"]], 2 * idx[R["metal_ok"]] + 1])
+    order = np.argsort(vr_key, kind="stable")
+    if len(vr_dev):
+        ii = vr_dev[order]
+        add(np.stack([M + ii, 5 * M + ii], 1), np.tile([bpf, -bpf], (len(ii), 1)), vr_rhs[order])
 
     # cycle rows, interleaved (row1_i, row2_i); busy coefficients = objective coefficients
     busy = S[:, :6]  # a, b, p1, p2, p3, pV
@@ -229,13 +306,14 @@ def lower_fleet(devs: Sequence[DeviceProfile], model: ModelProfile, kv_bits: str
     in_set = np.zeros((3, M), dtype=bool)
     for s, key in enumerate(("M1", "M2", "M3")):
         in_set[s, sets[key]] = True
-    gpu = np.array([bool(d.has_cuda and d.d_avail_cuda is not None) or bool(d.has_metal and d.d_avail_metal is not None)
-                    for d in devs], dtype=bool)
+    gpu = R["cuda_ok"] | R["metal_ok"]
 
     t_comm = 0
-    for d in devs:
-        t_comm += d.t_comm
-    xi_sum = sum(float(v) for v in xi)
+    for v in R["tcomm"]:
+        t_comm += v
+    xi_sum = 0
+    for v in xi.tolist():
+        xi_sum += v
 
     return FleetMILP(
         M=M, L=model.L, n_cols=N, n_rows=len(counts),
