@@ -56,12 +56,13 @@ enum { CLS_DONE = 0, CLS_K1 = 1, CLS_KC = 2 };  // screen verdicts
 //   cnt    per device row counter | have1 << 8 | have2 << 16
 //   st0/1  per device ints (DP backtracking states, ping-pong)
 //   rng    per DP-tree slot: finite range [lo, hi] of the node's sequence
+//   inc    per device next increment (greedy exchange)
 //   G      [i][e] table, row stride RS (odd), leaves of the DP tree; k = 1 reduces in place
 //   H      [i][e] least cycle time (k > 1 only)
 //   work   DP tree levels when the leaves must survive (k > 1 threshold scan)
 //   split  DP tree argmin (uint8 e of the left subtree), ~M * (R + 1) bytes
 struct Slice {
-    int64_t rows, cyc, cost, cnt, st0, st1, rng, G, H, work, split, total;
+    int64_t rows, cyc, cost, cnt, st0, st1, rng, inc, G, H, work, split, total;
 };
 
 __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -78,6 +79,7 @@ __host__ __device__ inline Slice make_slice(int mmax, int r1max, int tab, int ta
     s.st0 = o;   o = align16(o + int64_t(mmax) * 4);
     s.st1 = o;   o = align16(o + int64_t(mmax) * 4);
     s.rng = o;   o = align16(o + int64_t(mmax) * 8);
+    s.inc = o;   o = align16(o + int64_t(mmax) * 8);
     s.G = o;     o = align16(o + tmax * 8);
     s.H = o;     o = align16(o + int64_t(tab_kc) * 8);
     s.work = o;  o = align16(o + (tab_kc > 0 ? (int64_t(tab_kc) / 2 + 2 * int64_t(r1max) + 2) * 8 : 0));
@@ -308,6 +310,7 @@ struct WaveCtx {
     int *cnt;
     int *st0, *st1;
     int2 *rng;     // [slot] finite range of a DP-tree node (merge path)
+    double *inc;   // [i] next increment of device i (greedy exchange)
     double *G, *H, *work;
     uint8_t *split;
 };
@@ -356,33 +359,109 @@ __device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, 
     }
 }
 
+struct LeafInfo {
+    bool convex;  // every leaf's finite set is an interval and the leaf is convex on it
+    bool empty;   // some leaf has no allowed entry (the call is infeasible)
+    int lo_sum;   // sum of the leaves' first allowed e
+    int cap;      // sum of (hi - lo)
+};
+
 // Leaf pre-pass of one DP call (lane = device): finite range [lo, hi] of the
-// leaf A_i[e] = G[i][e] (+inf where H[i][e] > T when use_T) into rng[i], and
-// whether the merge path applies: the finite set is an interval and A_i is
-// convex on it (increments non-decreasing up to 1e-12 relative). The cost is
-// L-natural convex in (w, n), so G_i (its minimum over n) is convex in w and its
-// threshold sublevel sets are intervals; the check guards the floating point.
-__device__ bool leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, int lane) {
-    bool ok = true;
+// leaf A_i[e] = G[i][e] (+inf where H[i][e] > T when use_T) into rng[i]. The
+// cost is L-natural convex in (w, n), so G_i (its minimum over n) is convex in w
+// and its threshold sublevel sets are intervals; the check guards the floating
+// point (increments must not decrease by more than 1e-12 relative).
+__device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, int lane) {
+    bool ok = true, empty = false;
+    int lo_sum = 0, cap = 0;
     for (int i = lane; i < M; i += 64) {
         const double *G = w.G + int64_t(i) * RS, *H = w.H + int64_t(i) * RS;
         int lo = R1, hi = -1, cnt = 0;
+        double prev = kInf, dprev = -kInf;
         for (int e = 0; e < R1; ++e) {
-            const bool in = G[e] < kInf && (!use_T || H[e] <= T);
+            const double g = G[e];
+            const bool in = g < kInf && (!use_T || H[e] <= T);
             if (in) {
+                if (cnt > 0) {
+                    const double d = g - prev;
+                    ok = ok && (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
+                    dprev = d;
+                }
                 lo = min(lo, e);
                 hi = e;
+                prev = g;
                 ++cnt;
             }
         }
-        ok = ok && (cnt == 0 || cnt == hi - lo + 1);
-        for (int e = lo + 1; e < hi; ++e) {
-            const double d0 = G[e] - G[e - 1], d1 = G[e + 1] - G[e];
-            ok = ok && d1 >= d0 - 1e-12 * fmax(1.0, fabs(G[e]));
-        }
+        empty = empty || cnt == 0;
+        lo_sum += lo;
+        cap += hi - lo;
         w.rng[i] = make_int2(lo, hi);
     }
-    return !wave_or(!ok);
+    LeafInfo li;
+    li.convex = !wave_or(!ok);
+    li.empty = wave_or(empty);
+    li.lo_sum = wave_sum(lo_sum);
+    li.cap = wave_sum(cap);
+    return li;
+}
+
+// Separable convex allocation by the greedy exchange: start every device at its
+// first allowed e, then hand out the remaining R - sum(lo) layers one at a time
+// to the device whose next increment G_i[e+1] - G_i[e] is smallest (ties ->
+// lowest device index). Optimal because every leaf is convex on its interval.
+// The wave is the priority queue: one wave_min per step. Leaves e_i in st0.
+__device__ double greedy_alloc(const WaveCtx &w, int M, int R1, int RS, const LeafInfo &li, int lane) {
+    int need = (R1 - 1) - li.lo_sum;
+    if (li.empty || need < 0 || need > li.cap) return kInf;
+    for (int i = lane; i < M; i += 64) {
+        const int2 r = w.rng[i];
+        const double *G = w.G + int64_t(i) * RS;
+        w.st0[i] = r.x;
+        w.inc[i] = r.x < r.y ? G[r.x + 1] - G[r.x] : kInf;
+    }
+    wave_sync();
+    // Rounds: the device with the smallest next increment (ties -> lowest index)
+    // takes every further increment that still beats the runner-up, so a round
+    // equals a run of one-at-a-time greedy steps.
+    while (need > 0) {
+        double bv = kInf, sv = kInf;
+        int bi = 0x7fffffff, si = 0x7fffffff;
+        for (int i = lane; i < M; i += 64) {
+            const double v = w.inc[i];
+            if (v < bv) { sv = bv; si = bi; bv = v; bi = i; }
+            else if (v < sv) { sv = v; si = i; }
+        }
+        const double m = wave_min(bv);
+        int win = bv == m ? bi : 0x7fffffff;
+        for (int o = 32; o > 0; o >>= 1) win = min(win, __shfl_xor(win, o));
+        const int wl = win & 63;
+        const double rv = lane == wl ? sv : bv;
+        const int ri = lane == wl ? si : bi;
+        const double m2 = wave_min(rv);
+        int d2 = rv == m2 ? ri : 0x7fffffff;
+        for (int o = 32; o > 0; o >>= 1) d2 = min(d2, __shfl_xor(d2, o));
+        int t = 0;
+        if (lane == wl) {
+            int e = w.st0[win];
+            const int hi = w.rng[win].y;
+            const double *G = w.G + int64_t(win) * RS;
+            while (t < need && e < hi) {
+                const double x = G[e + 1] - G[e];
+                if (!(x < m2 || (x == m2 && win < d2))) break;
+                ++e;
+                ++t;
+            }
+            w.st0[win] = e;
+            w.inc[win] = e < hi ? G[e + 1] - G[e] : kInf;
+        }
+        need -= __shfl(t, wl);
+        wave_sync();
+    }
+    double S = 0.0;
+    for (int i = lane; i < M; i += 64) S += w.G[int64_t(i) * RS + w.st0[i]];
+    for (int o = 32; o > 0; o >>= 1) S += __shfl_xor(S, o);
+    return S;
 }
 
 // Tree min-plus DP over the devices. Leaves: A_i[e] = G[i][e] (masked to +inf
@@ -500,13 +579,6 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
     return buf[R1 - 1];
 }
 
-// One DP call: leaf ranges / convexity check, then the tree.
-__device__ double dp_call(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
-    const bool convex = M > 1 && leaf_ranges(w, M, R1, RS, use_T, T, lane);
-    wave_sync();
-    return tree_dp(w, M, R1, RS, use_T, T, buf, lane, convex);
-}
-
 // Walk the tree top-down from the root state R: st0[i] = e_i of device i.
 __device__ void tree_backtrack(const WaveCtx &w, int M, int R1, int lane) {
     if (M == 1) {
@@ -545,6 +617,23 @@ __device__ void tree_backtrack(const WaveCtx &w, int M, int R1, int lane) {
         for (int i = lane; i < M; i += 64) w.st0[i] = cur[i];
         wave_sync();
     }
+}
+
+// One DP call: leaf ranges / convexity check, then the greedy exchange (convex
+// leaves, few layers to hand out) or the tree; leaves the chosen e_i in st0 and
+// returns the minimum (+inf when infeasible).
+__device__ double dp_call(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
+    if (M > 1) {
+        const LeafInfo li = leaf_ranges(w, M, R1, RS, use_T, T, lane);
+        wave_sync();
+        if (li.convex && (R1 - 1) - li.lo_sum <= 48) return greedy_alloc(w, M, R1, RS, li, lane);
+        const double v = tree_dp(w, M, R1, RS, use_T, T, buf, lane, li.convex);
+        if (v < kInf) tree_backtrack(w, M, R1, lane);
+        return v;
+    }
+    const double v = tree_dp(w, M, R1, RS, use_T, T, buf, lane, false);
+    if (v < kInf) tree_backtrack(w, M, R1, lane);
+    return v;
 }
 
 struct Inst {
@@ -739,23 +828,28 @@ __device__ int check_rows(const WaveCtx &w, int M, int lane) {
     return bad;
 }
 
-// Table pass (lane = device): G[i][e] (and H[i][e] for k > 1), w = lb + e.
+// One table entry e of device i, continuing the chain state (n, have).
+__device__ inline void table_entry(const Dev &d, const WaveCtx &w, const Inst &I, int i, int e, int &n, bool &have) {
+    const int wl = d.wlo + e;
+    int s[4];
+    double g = kInf, h = kInf;
+    bool ok = false;
+    if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
+    if (ok && I.kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
+    have = ok;
+    w.G[i * I.RS + e] = ok ? g : kInf;
+    if (I.kc > 0.0) w.H[i * I.RS + e] = h;
+}
+
+// Table pass (lane = device): G[i][e] (and H[i][e] for k > 1), w = lb + e, one
+// incremental chain per device (split_step reuses the previous argmin).
 __device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane) {
     for (int i = lane; i < I.M; i += 64) {
         Dev d;
         load_dev(d, B, w, I.co, I.M, i, I.Wd);
-        int n = 0, s[4];
+        int n = 0;
         bool have = false;
-        for (int e = 0; e < I.R1; ++e) {
-            const int wl = d.wlo + e;
-            double g = kInf, h = kInf;
-            bool ok = false;
-            if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
-            if (ok && I.kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
-            have = ok;
-            w.G[i * I.RS + e] = ok ? g : kInf;
-            if (I.kc > 0.0) w.H[i * I.RS + e] = h;
-        }
+        for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
     }
 }
 
@@ -777,8 +871,7 @@ __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &node
         if (phase == 0) {
             s_inf = st;
             if (!(st < kInf)) return false;
-            if (!(kc > 0.0)) break;  // k = 1: the splits of this pass are final
-            tree_backtrack(w, M, R1, lane);
+            if (!(kc > 0.0)) break;  // k = 1: the allocation of this pass is final
             double hmax = 0.0;
             for (int i = lane; i < M; i += 64) {
                 hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
@@ -809,13 +902,12 @@ __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &node
                 T = t;
                 continue;
             }
-            if (!use_T && !(bestT < kInf)) break;  // no scan pass ran: phase-0 splits are final
+            if (!use_T && !(bestT < kInf)) break;  // no scan pass ran: the phase-0 allocation is final
             phase = 2;
             use_T = bestT < kInf;
             T = bestT;
         }
     }
-    tree_backtrack(w, M, R1, lane);
     return true;
 }
 
@@ -891,6 +983,7 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
     w.st0 = reinterpret_cast<int *>(smem + sl.st0);
     w.st1 = reinterpret_cast<int *>(smem + sl.st1);
     w.rng = reinterpret_cast<int2 *>(smem + sl.rng);
+    w.inc = reinterpret_cast<double *>(smem + sl.inc);
     w.G = reinterpret_cast<double *>(smem + sl.G);
     w.H = reinterpret_cast<double *>(smem + sl.H);
     w.work = reinterpret_cast<double *>(smem + sl.work);
