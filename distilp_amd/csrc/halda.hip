@@ -93,22 +93,17 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ inline double wave_min(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ inline double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ inline int wave_or(int v) {
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
-    return v;
-}
-__device__ inline int wave_sum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+// Wave reductions over the active lanes (DPP, result uniform) from the device library.
+extern "C" __device__ double __ockl_wfred_min_f64(double);
+extern "C" __device__ double __ockl_wfred_max_f64(double);
+extern "C" __device__ int __ockl_wfred_min_i32(int);
+extern "C" __device__ int __ockl_wfred_or_i32(int);
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+__device__ inline double wave_min(double v) { return __ockl_wfred_min_f64(v); }
+__device__ inline double wave_max(double v) { return __ockl_wfred_max_f64(v); }
+__device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
+__device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
+__device__ inline int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
 
 __device__ inline void write_done(const halda_result &R, int inst, int status, int64_t nodes) {
     R.status[inst] = status;
@@ -121,60 +116,115 @@ __device__ inline void write_done(const halda_result &R, int inst, int status, i
 __host__ __device__ inline int odd_stride(int r1) { return r1 | 1; }
 
 // ---------------------------------------------------------------- screen
-// One wave per instance. Settles everything decidable from the equality row and
-// the w bounds (non-HALDA shape, bound infeasibility such as M > W = L/k) and
-// flags the rest for the solve kernel (class 1: c[C] == 0, class 2: c[C] > 0).
+// One wave screens kScreenPer consecutive instances. Settles everything
+// decidable from the equality row and the w bounds (non-HALDA shape, bound
+// infeasibility such as M > W = L/k) and flags the rest for the solve kernel
+// (class 1: c[C] == 0, class 2: c[C] > 0). The loads of all its instances are
+// issued together: headers (lane g = instance g), then equality-row extents and
+// bounds (lane g), then per instance the equality row and w bounds (lane =
+// device), so a wave spends three memory round trips on kScreenPer instances.
+constexpr int kScreenPer = 8;
+
+__device__ inline int64_t shfl64(int64_t v, int src) {
+    const int lo = __shfl(int(uint32_t(uint64_t(v))), src), hi = __shfl(int(uint32_t(uint64_t(v) >> 32)), src);
+    return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+}
+
 __global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls,
                                                                 int mmax, int r1max, int tab, int tab_kc) {
     const int lane = threadIdx.x & 63;
-    const int inst = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (inst >= B.n_inst) return;
-    const int N = B.n_cols[inst], m = B.n_rows[inst];
+    const int64_t i0 = (int64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6)) * kScreenPer;
+    if (i0 >= B.n_inst) return;
+    // lane g < kScreenPer: header of instance i0 + g
+    const int64_t my = i0 + lane;
+    const bool own = lane < kScreenPer && my < B.n_inst;
+    int N = 1, m = 1;
+    int64_t co = 0, ro = 0, cs = 0;
+    if (own) {
+        N = B.n_cols[my];
+        m = B.n_rows[my];
+        co = B.col_off[my];
+        ro = B.row_off[my];
+        cs = B.csr_off[my];
+    }
     int status = 0;  // 0 = still open
     if (N < 1 || (N - 1) % 7 != 0 || m < 1) status = HALDA_STATUS_UNSUPPORTED;
-    const int M = (N - 1) / 7;
+    const int M = status ? 0 : (N - 1) / 7;
     if (!status && M > mmax) status = HALDA_STATUS_TOO_LARGE;
-    if (!status) {
-        const int64_t co = B.col_off[inst], ro = B.row_off[inst];
-        const int32_t *rp = B.row_ptr + B.csr_off[inst];
-        const double Wd = B.row_ub[ro + m - 1];
-        const int eqs = rp[m - 1], eqe = rp[m];
-        if (!(B.row_lb[ro + m - 1] == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M) {
-            status = HALDA_STATUS_UNSUPPORTED;
-        } else {
-            const int W = int(Wd);
-            int bad = 0, infeas = 0, sumlo = 0;
-            for (int i = lane; i < M; i += 64) {
-                bad |= B.col_idx[eqs + i] != i || B.val[eqs + i] != 1.0;
-                const double lb = B.col_lb[co + i], ub = B.col_ub[co + i];
-                const int wlo = int(ceil(lb)), whi = int(floor(fmin(ub, Wd)));
-                infeas |= wlo > whi || lb < 0.0;
-                sumlo += wlo;
-            }
-            bad = wave_or(bad);
-            infeas = wave_or(infeas);
-            sumlo = wave_sum(sumlo);
-            if (bad) status = HALDA_STATUS_UNSUPPORTED;
-            else if (infeas || sumlo > W || (M == 0 && W > 0)) status = HALDA_STATUS_INFEASIBLE;
-            else if (M == 0) {  // no devices and W = 0: x = [C = 0] is optimal
-                if (lane == 0) {
-                    cls[inst] = CLS_DONE;
-                    Rz.x[co] = 0.0;
-                    Rz.status[inst] = HALDA_STATUS_OPTIMAL;
-                    Rz.obj_lin[inst] = Rz.dual_bound[inst] = Rz.gap[inst] = 0.0;
-                    Rz.nodes[inst] = 0;
-                }
-            } else {
-                const int R1 = W - sumlo + 1;
-                const bool kc = B.c[co + 7 * M] > 0.0;
-                if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
-                else if (lane == 0) cls[inst] = kc ? CLS_KC : CLS_K1;
-            }
+    int eqs = 0, eqe = 0;
+    double Wd = 0.0, Wl = 0.0, cC = 0.0;
+    if (own && !status) {
+        const int32_t *rp = B.row_ptr + cs;
+        eqs = rp[m - 1];
+        eqe = rp[m];
+        Wd = B.row_ub[ro + m - 1];
+        Wl = B.row_lb[ro + m - 1];
+        cC = B.c[co + 7 * int64_t(M)];
+    }
+    if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
+        status = HALDA_STATUS_UNSUPPORTED;
+
+    // per instance g (lane = device): equality row entries and w bounds, all issued first
+    int cv[kScreenPer];
+    double vv[kScreenPer], lbv[kScreenPer], ubv[kScreenPer];
+#pragma unroll
+    for (int g = 0; g < kScreenPer; ++g) {
+        const int Mg = __shfl(M, g), stg = __shfl(status, g), eg = __shfl(eqs, g);
+        const int64_t cg = shfl64(co, g);
+        const bool in = i0 + g < B.n_inst && stg == 0 && lane < Mg;
+        cv[g] = in ? B.col_idx[eg + lane] : lane;
+        vv[g] = in ? B.val[eg + lane] : 1.0;
+        lbv[g] = in ? B.col_lb[cg + lane] : 0.0;
+        ubv[g] = in ? B.col_ub[cg + lane] : 0.0;
+    }
+    int verdict = CLS_DONE, vstatus = status;  // lane g: outcome of instance g
+#pragma unroll
+    for (int g = 0; g < kScreenPer; ++g) {
+        if (i0 + g >= B.n_inst) break;
+        const int stg = __shfl(status, g);
+        if (stg) continue;
+        const int Mg = __shfl(M, g), eg = __shfl(eqs, g);
+        const int64_t cg = shfl64(co, g);
+        const double Wg = __shfl(Wd, g);
+        int bad = 0, infeas = 0, sumlo = 0;
+        auto one = [&](int i, int col, double v, double lb, double ub) {
+            bad |= col != i || v != 1.0;
+            const int wlo = int(ceil(lb)), whi = int(floor(fmin(ub, Wg)));
+            infeas |= wlo > whi || lb < 0.0;
+            sumlo += wlo;
+        };
+        if (lane < Mg) one(lane, cv[g], vv[g], lbv[g], ubv[g]);
+        for (int i = lane + 64; i < Mg; i += 64) one(i, B.col_idx[eg + i], B.val[eg + i], B.col_lb[cg + i], B.col_ub[cg + i]);
+        bad = wave_or(bad | (infeas << 1));
+        sumlo = wave_sum(sumlo);
+        const int W = int(Wg);
+        int st = 0, v = CLS_DONE;
+        if (bad & 1) st = HALDA_STATUS_UNSUPPORTED;
+        else if ((bad & 2) || sumlo > W || (Mg == 0 && W > 0)) st = HALDA_STATUS_INFEASIBLE;
+        else if (Mg == 0) st = HALDA_STATUS_OPTIMAL;  // no devices and W = 0: x = [C = 0]
+        else {
+            const int R1 = W - sumlo + 1;
+            const bool kc = __shfl(cC, g) > 0.0;
+            if (R1 > r1max || int64_t(Mg) * odd_stride(R1) > (kc ? tab_kc : tab)) st = HALDA_STATUS_TOO_LARGE;
+            else v = kc ? CLS_KC : CLS_K1;
+        }
+        if (lane == g) {
+            vstatus = st;
+            verdict = v;
         }
     }
-    if (status && lane == 0) {
-        cls[inst] = CLS_DONE;
-        write_done(Rz, inst, status, 0);
+    if (own) {
+        cls[my] = uint8_t(verdict);
+        if (verdict == CLS_DONE) {
+            if (vstatus == HALDA_STATUS_OPTIMAL) {
+                Rz.x[co] = 0.0;
+                Rz.status[my] = HALDA_STATUS_OPTIMAL;
+                Rz.obj_lin[my] = Rz.dual_bound[my] = Rz.gap[my] = 0.0;
+                Rz.nodes[my] = 0;
+            } else {
+                write_done(Rz, int(my), vstatus, 0);
+            }
+        }
     }
 }
 
@@ -433,14 +483,12 @@ __device__ double greedy_alloc(const WaveCtx &w, int M, int R1, int RS, const Le
             else if (v < sv) { sv = v; si = i; }
         }
         const double m = wave_min(bv);
-        int win = bv == m ? bi : 0x7fffffff;
-        for (int o = 32; o > 0; o >>= 1) win = min(win, __shfl_xor(win, o));
+        const int win = wave_imin(bv == m ? bi : 0x7fffffff);
         const int wl = win & 63;
         const double rv = lane == wl ? sv : bv;
         const int ri = lane == wl ? si : bi;
         const double m2 = wave_min(rv);
-        int d2 = rv == m2 ? ri : 0x7fffffff;
-        for (int o = 32; o > 0; o >>= 1) d2 = min(d2, __shfl_xor(d2, o));
+        const int d2 = wave_imin(rv == m2 ? ri : 0x7fffffff);
         int t = 0;
         if (lane == wl) {
             int e = w.st0[win];
@@ -455,7 +503,7 @@ __device__ double greedy_alloc(const WaveCtx &w, int M, int R1, int RS, const Le
             w.st0[win] = e;
             w.inc[win] = e < hi ? G[e + 1] - G[e] : kInf;
         }
-        need -= __shfl(t, wl);
+        need -= __builtin_amdgcn_readlane(t, wl);
         wave_sync();
     }
     double S = 0.0;
@@ -1098,7 +1146,8 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     }
     uint8_t *cls = static_cast<uint8_t *>(ctx->work);
     HIP_TRY(hipEventRecord(ctx->ev0, stream));
-    hipLaunchKernelGGL(halda_screen_kernel, dim3((in.n_inst + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0,
+    const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
+    hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
                        stream, in, out, cls, mmax, in.max_R1, int(tab), int(tab_kc));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->evs, stream));
