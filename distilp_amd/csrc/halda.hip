@@ -45,8 +45,9 @@ constexpr int kRows = 4;            // capacity rows per device (link, RAM/Metal
 constexpr int kMaxRowNnz = 8;       // widest HALDA row (cycle rows: 6 device cols + z + C)
 constexpr double kSlackEps = 1e-9;  // a capacity row counts as met within 1e-9 layers (oracle: same)
 constexpr double kInf = __builtin_huge_val();
+constexpr int kK1MaxM = 64;         // widest fleet the k = 1 fast path takes (lane = device)
 
-enum { CLS_DONE = 0, CLS_K1 = 1, CLS_KC = 2 };  // screen verdicts
+enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2 };  // screen verdicts: settled / k = 1 fast path / general kernel
 
 // ---------------------------------------------------------------- LDS slice
 // One solve wave = one 64-thread workgroup with its own LDS slice (bytes):
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, hal
             const int R1 = W - sumlo + 1;
             const bool kc = __shfl(cC, g) > 0.0;
             if (R1 > r1max || int64_t(Mg) * odd_stride(R1) > (kc ? tab_kc : tab)) st = HALDA_STATUS_TOO_LARGE;
-            else v = kc ? CLS_KC : CLS_K1;
+            else v = (kc || Mg > kK1MaxM) ? CLS_GEN : CLS_K1;
         }
         if (lane == g) {
             vstatus = st;
@@ -1042,7 +1043,7 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
     const int S = gridDim.x;
     for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
         const int64_t mine = base + int64_t(lane) * S;
-        const bool open = mine < B.n_inst && cls[mine] != CLS_DONE;
+        const bool open = mine < B.n_inst && cls[mine] == CLS_GEN;
         uint64_t todo = __ballot(open);
         while (todo) {
             const int bit = __builtin_ctzll(todo);
@@ -1092,6 +1093,242 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
     }
 }
 
+// ---------------------------------------------------------------- k = 1 fast path
+// c[C] == 0 and M <= 64 (every feasible C3 instance): the cycle rows never bind,
+// the problem is min sum_i G_i(e_i) s.t. sum e_i = R with G_i convex, and the
+// greedy exchange is exact. No tables: lane i holds device i's record in
+// registers and only G_i(0), G_i(1). Each round the device with the smallest
+// next increment (ties -> lowest index) wins; the whole wave then evaluates the
+// winner's G at its next 64 layer counts in parallel (its record broadcast from
+// the winner lane through readlane), and the winner keeps every increment that
+// still beats the runner-up's -- one round usually places all R layers, where
+// the table path evaluates M x (R + 1) entries. The convexity the exchange
+// relies on is re-checked on every evaluated window (same 1e-12 tolerance as
+// leaf_ranges); an instance whose leaves do not start at e = 0 or fail the
+// check is handed to the general kernel (cls = CLS_GEN), never approximated.
+
+struct K1Slice {
+    int64_t rows, cyc, cost, cnt, total;
+};
+
+__host__ __device__ inline K1Slice make_k1_slice(int mmax) {
+    K1Slice s;
+    int64_t o = 0;
+    s.rows = o; o = align16(o + int64_t(mmax) * kRows * 8);
+    s.cyc = o;  o = align16(o + int64_t(mmax) * 4 * 8);
+    s.cost = o; o = align16(o + int64_t(mmax) * 6 * 8);
+    s.cnt = o;  o = align16(o + int64_t(mmax) * 4);
+    s.total = o;
+    return s;
+}
+
+// Record of lane `src` broadcast to the whole wave (src wave-uniform).
+__device__ inline double bcast(double v, int src) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane(int(uint32_t(u)), src);
+    const uint32_t hi = __builtin_amdgcn_readlane(int(uint32_t(u >> 32)), src);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+__device__ inline int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+
+__device__ inline Dev bcast_dev(const Dev &d, int src) {
+    Dev o;
+    o.cw = bcast(d.cw, src); o.cn = bcast(d.cn, src);
+    o.cs0 = bcast(d.cs0, src); o.cs1 = bcast(d.cs1, src); o.cs2 = bcast(d.cs2, src); o.cs3 = bcast(d.cs3, src);
+    o.r1w = bcast(d.r1w, src); o.r2w = bcast(d.r2w, src); o.rhs1 = bcast(d.rhs1, src); o.rhs2 = bcast(d.rhs2, src);
+    o.wlo = bcast(d.wlo, src); o.whi = bcast(d.whi, src); o.nlo = bcast(d.nlo, src); o.nhi = bcast(d.nhi, src);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        o.slo[j] = bcast(d.slo[j], src); o.shi[j] = bcast(d.shi[j], src);
+        o.us[j] = bcast(d.us[j], src); o.vs[j] = bcast(d.vs[j], src); o.Ks[j] = bcast(d.Ks[j], src);
+    }
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        o.uf[f] = bcast(d.uf[f], src); o.vf[f] = bcast(d.vf[f], src); o.Kf[f] = bcast(d.Kf[f], src);
+    }
+    return o;
+}
+
+__device__ inline double shfl_up1(double v, int lane) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int src = lane > 0 ? lane - 1 : 0;
+    const uint32_t lo = __shfl(int(uint32_t(u)), src), hi = __shfl(int(uint32_t(u >> 32)), src);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+
+__device__ inline double wave_sum_f64(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
+
+// Greedy exchange over lazily evaluated convex leaves (lane = device, M <= 64).
+// On K1_OK, e holds the device's extra layers.
+__device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &rounds) {
+    const bool act = lane < M;
+    double g0 = kInf, g1 = kInf;
+    int n0 = 0, n1 = 0, s[4];
+    bool ok0 = false, ok1 = false;
+    if (act) {
+        ok0 = d.wlo <= d.whi && split_full(d, d.wlo, g0, n0, s);
+        ok1 = ok0 && d.wlo + 1 <= d.whi && split_step(d, d.wlo + 1, n0, g1, n1, s);
+    }
+    e = 0;
+    // every leaf must start at e = 0 (a later start is legal but rare: general kernel)
+    if (wave_or(act && !ok0)) return K1_FALLBACK;
+    double gn = ok1 ? g1 : kInf;               // G(e + 1)
+    double inc = ok1 ? g1 - g0 : kInf;        // G(e + 1) - G(e)
+    double dprev = -kInf;                      // last taken increment (convexity check)
+    int need = R;
+    rounds = 0;
+    while (need > 0) {
+        ++rounds;
+        const double bv = wave_min(act ? inc : kInf);
+        if (!(bv < kInf)) return K1_INFEASIBLE;  // no device can take another layer
+        const int win = wave_imin(act && inc == bv ? lane : 0x7fffffff);
+        const double rv = act && lane != win ? inc : kInf;
+        const double m2 = wave_min(rv);
+        const int d2 = wave_imin(act && lane != win && rv == m2 ? lane : 0x7fffffff);
+        const int ew = bcast(e, win);
+        const double gnw = bcast(gn, win), dpw = bcast(dprev, win);
+        // the winner takes its next increment bv; lane t evaluates G_win(ew + 2 + t)
+        int take = 1;
+        bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
+        double Gt = kInf, dt = kInf;
+        if (need > 1) {
+            const Dev dw = bcast_dev(d, win);
+            const int wl = dw.wlo + ew + 2 + lane;
+            double g = kInf;
+            int nn = 0;
+            if (wl <= dw.whi && split_full(dw, wl, g, nn, s)) Gt = g;
+            // shuffles on the full wave first (a bpermute under a lane-0-off mask would read 0 there)
+            const double up = shfl_up1(Gt, lane);
+            const double prev = lane == 0 ? gnw : up;
+            dt = Gt - prev;  // increment ew + 1 + lane -> ew + 2 + lane
+            const double dup = shfl_up1(dt, lane);
+            const double dlast = lane == 0 ? bv : dup;
+            const bool fin = Gt < kInf && prev < kInf;
+            const bool beats = fin && (dt < m2 || (dt == m2 && win < d2));
+            const uint64_t nb = __ballot(!beats);
+            const int run = nb ? __builtin_ctzll(nb) : 64;  // increments after the first that still win
+            take = min(min(1 + run, need), 64);
+            // convexity over the increments taken and the next one (they decide the exchange)
+            bad = bad || wave_or(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt)));
+        }
+        if (bad) return K1_FALLBACK;
+        // winner's new state: e = ew + take; G(e) and G(e + 1) from the evaluated window
+        const double gcur = take == 1 ? gnw : bcast(Gt, take - 2);
+        const double gnext = need > 1 ? bcast(Gt, take - 1) : kInf;
+        const double tlast = take == 1 ? bv : bcast(dt, take - 2);
+        if (lane == win) {
+            e = ew + take;
+            gn = gnext;
+            inc = gnext < kInf ? gnext - gcur : kInf;
+            dprev = tlast;
+        }
+        need -= take;
+    }
+    return K1_OK;
+}
+
+#ifndef HALDA_K1_WAVES_PER_SIMD
+#define HALDA_K1_WAVES_PER_SIMD 4  // occupancy target of the k = 1 kernel (register budget)
+#endif
+
+__global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_kernel(halda_batch B, halda_result Rz,
+                                                                                      uint8_t *cls, int mmax) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
+    WaveCtx w = {};
+    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
+    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
+    w.cost = reinterpret_cast<double *>(smem + sl.cost);
+    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
+    const int S = gridDim.x;
+    for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
+        const int64_t mine = base + int64_t(lane) * S;
+        uint64_t todo = __ballot(mine < B.n_inst && cls[mine] == CLS_K1);
+        while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            Inst I;
+            I.inst = int(base + int64_t(bit) * S);
+            const int N = B.n_cols[I.inst];
+            I.m = B.n_rows[I.inst];
+            I.M = (N - 1) / 7;
+            I.iC = 7 * I.M;
+            I.invM = 1.0f / float(I.M);
+            I.co = B.col_off[I.inst];
+            I.ro = B.row_off[I.inst];
+            I.rp = B.row_ptr + B.csr_off[I.inst];
+            I.Wd = B.row_ub[I.ro + I.m - 1];
+            I.W = int(I.Wd);
+            I.kc = B.c[I.co + I.iC];
+            HALDA_STAMP(0);
+            int bad = 0;
+            const int sumlo = device_pass(B, w, I, lane, bad);
+            wave_sync();
+            HALDA_STAMP(1);
+            bad |= row_pass(B, w, I, lane);
+            wave_sync();
+            HALDA_STAMP(2);
+            bad |= check_rows(w, I.M, lane);
+            if (wave_or(bad)) {
+                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
+                continue;
+            }
+            HALDA_STAMP(3);
+            Dev d = {};
+            if (lane < I.M) load_dev(d, B, w, I.co, I.M, lane, I.Wd);
+            HALDA_STAMP(4);
+            int e = 0, rounds = 0;
+            const int rc = k1_alloc(d, I.M, I.W - sumlo, lane, e, rounds);
+            wave_sync();  // LDS records are rewritten by the next instance
+            HALDA_STAMP(5);
+            if (rc == K1_FALLBACK) {
+                if (lane == 0) cls[I.inst] = CLS_GEN;
+                continue;
+            }
+            if (rc == K1_INFEASIBLE) {
+                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_INFEASIBLE, 1);
+                continue;
+            }
+            double g = 0.0, H = 0.0;
+            if (lane < I.M) {
+                const int wl = d.wlo + e;
+                double P, Q;
+                int n = 0, s[4] = {0, 0, 0, 0};
+                split_full(d, wl, g, n, s);
+                dev_cycle(d, wl, n, s, P, Q);
+                double *x = Rz.x + I.co;
+                const int M = I.M;
+                x[lane] = double(wl);
+                x[M + lane] = double(n);
+                x[2 * M + lane] = double(s[0]);
+                x[3 * M + lane] = double(s[1]);
+                x[4 * M + lane] = double(s[2]);
+                x[5 * M + lane] = double(s[3]);
+                x[6 * M + lane] = Q > P ? 0.5 * (Q - P) : 0.0;
+                H = Q >= P ? 0.5 * (P + Q) : P;
+            }
+            const double hmax = fmax(0.0, wave_max(lane < I.M ? H : 0.0));
+            const double gsum = wave_sum_f64(lane < I.M ? g : 0.0);
+            if (lane == 0) {
+                const double obj = gsum + I.kc * hmax;
+                Rz.x[I.co + I.iC] = hmax;
+                Rz.status[I.inst] = HALDA_STATUS_OPTIMAL;
+                Rz.obj_lin[I.inst] = obj;
+                Rz.dual_bound[I.inst] = obj;
+                Rz.gap[I.inst] = 0.0;
+                Rz.nodes[I.inst] = rounds;
+            }
+            HALDA_STAMP(6);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host side
 thread_local std::string g_err;
 
@@ -1110,7 +1347,7 @@ struct Ctx {
     int device = 0;
     int cus = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr;  // launch start, end, solve-kernel start
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after screen, after k=1 kernel
     bool timed = false;
     void *scratch = nullptr;  // host-API staging
     size_t scratch_bytes = 0;
@@ -1151,6 +1388,18 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
                        stream, in, out, cls, mmax, in.max_R1, int(tab), int(tab_kc));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->evs, stream));
+    // k = 1 fast path: small LDS slice (device records only), high occupancy
+    {
+        const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, halda_solve_k1_kernel, 64, size_t(lds1)));
+        per_cu = std::max(1, per_cu);
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
+        hipLaunchKernelGGL(halda_solve_k1_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls, mmax);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(ctx->evk, stream));
+    // general kernel: k > 1, fleets wider than 64, and k = 1 instances the fast path handed over
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(halda_solve_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     // persistent grid: exactly the resident capacity (one 64-thread workgroup = one wave)
@@ -1202,7 +1451,7 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->evs) != hipSuccess) {
+        hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess) {
         delete c;
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
@@ -1219,6 +1468,7 @@ void halda_free(void *ctx) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evs) (void)hipEventDestroy(c->evs);
+    if (c->evk) (void)hipEventDestroy(c->evk);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1250,6 +1500,21 @@ int halda_last_solve_kernel_ms(void *ctx, double *ms) {
     float f = 0.f;
     HIP_TRY(hipEventElapsedTime(&f, c->evs, c->ev1));
     *ms = f;
+    return HALDA_OK;
+}
+
+int halda_last_phase_ms(void *ctx, double *ms3) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !ms3) return fail(HALDA_E_ARG, "NULL ctx/ms");
+    if (!c->timed) return fail(HALDA_E_ARG, "no solve has been launched on this context");
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float a = 0.f, b = 0.f, d = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evs));
+    HIP_TRY(hipEventElapsedTime(&b, c->evs, c->evk));
+    HIP_TRY(hipEventElapsedTime(&d, c->evk, c->ev1));
+    ms3[0] = a;
+    ms3[1] = b;
+    ms3[2] = d;
     return HALDA_OK;
 }
 

@@ -75,7 +75,7 @@ class HaldaResultC(ctypes.Structure):
 
 
 EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
-           "halda_last_solve_kernel_ms", "halda_lds_bytes", "halda_last_error", "halda_free")
+           "halda_last_solve_kernel_ms", "halda_last_phase_ms", "halda_lds_bytes", "halda_last_error", "halda_free")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -104,6 +104,8 @@ def load_library(path: Path | str | None = None):
         lib.halda_last_kernel_ms.restype = ctypes.c_int
         lib.halda_last_solve_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.halda_last_solve_kernel_ms.restype = ctypes.c_int
+        lib.halda_last_phase_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        lib.halda_last_phase_ms.restype = ctypes.c_int
         lib.halda_lds_bytes.argtypes = [ctypes.c_int32] * 4
         lib.halda_lds_bytes.restype = ctypes.c_int64
         lib.halda_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
@@ -248,6 +250,14 @@ class HaldaContext:
         if rc != 0:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
+
+    def last_phase_ms(self) -> Dict[str, float]:
+        """Device time of each launch of the last solve: screen, k = 1 fast path, general kernel."""
+        ms = (ctypes.c_double * 3)()
+        rc = self.lib.halda_last_phase_ms(self.ctx, ms)
+        if rc != 0:
+            raise RuntimeError(f"halda_last_phase_ms failed ({rc}): {last_error(self.lib)}")
+        return {"halda_screen_kernel": ms[0], "halda_solve_k1_kernel": ms[1], "halda_solve_kernel": ms[2]}
 
 
 _contexts: Dict[int, HaldaContext] = {}

@@ -116,8 +116,12 @@ int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out
 /* Device time of the last solve's kernel sequence (screen + compact + solve) in ms. */
 int halda_last_kernel_ms(void *ctx, double *ms);
 
-/* Device time of the last solve's main kernel (halda_solve_kernel) alone, in ms. */
+/* Device time of the last solve's solve kernels (k = 1 fast path + general), in ms. */
 int halda_last_solve_kernel_ms(void *ctx, double *ms);
+
+/* Device time of the last solve per launch, in ms: ms3[0] screen kernel,
+ * ms3[1] k = 1 fast-path kernel, ms3[2] general solve kernel. */
+int halda_last_phase_ms(void *ctx, double *ms3);
 
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc);

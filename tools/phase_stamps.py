@@ -40,6 +40,8 @@ def main():
     d = np.diff(st[:, :7], axis=1)
     d[:, 2] = st[:, 3] - st[:, 2]
     tot = st[:, 6] - st[:, 0]
+    nodes = res.nodes[:n][ok]
+    print("nodes (DP passes / greedy rounds): median", np.median(nodes), "max", nodes.max(), "mean", nodes.mean())
     print(f"instances {len(st)}  median total {np.median(tot):.0f} cycles")
     for j, nm in enumerate(names):
         print(f"  {nm:8s} median {np.median(d[:, j]):9.0f}  mean {d[:, j].mean():9.0f}  share {d[:, j].sum() / tot.sum():.3f}")
