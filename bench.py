@@ -56,20 +56,20 @@ def build_workload(rank: int, fleets: int, M: int):
 
 
 def algorithmic_bytes(lowered, batch, refs):
-    """Bytes each kernel of one launch sequence must move.
+    """Bytes each kernel of one launch sequence must move, as (k1_solve, screen).
 
-    solve kernel (the dominant one): for every instance that survives the screen, its fleet's CSR
-    (row_ptr + col_idx/val; counted once per fleet), its c / col_lb / col_ub (8 B each) and
+    k = 1 kernel (the dominant one): for every instance that survives the screen, its fleet's CSR
+    (row_ptr + col_idx/val; counted once per fleet), its header, c / col_lb / col_ub (8 B each) and
     integrality (1 B) per column, row_lb / row_ub per row, x out and the result scalars;
     screen kernel: for every instance its header (n_cols, n_rows, 3 offsets), the equality row
-    (two row_ptr entries, M col_idx/val, its row bounds), lb/ub of the M w-columns and c[C],
-    plus the result scalars of the instances it settles."""
+    (two row_ptr entries, M col_idx/val, its row bounds), lb/ub of the M w-columns and c[C], the
+    verdict byte, plus the result scalars of the instances it settles."""
     hdr, res = 4 + 4 + 8 + 8 + 8, 4 + 8 + 8 + 8 + 8
     solve, screen = 0, 0
     fleets_solved = set()
     for ref in refs:
         fl = lowered[ref.fleet]
-        screen += hdr + 8 + 12 * fl.M + 16 + 16 * fl.M + 8
+        screen += hdr + 8 + 12 * fl.M + 16 + 16 * fl.M + 8 + 1
         if ref.W - fl.M >= 0:
             if ref.fleet not in fleets_solved:
                 fleets_solved.add(ref.fleet)
@@ -249,8 +249,8 @@ def main():
     total_inst = batch.n_inst * world * args.steps
     value = total_inst / elapsed
     alg_solve, alg_screen = algorithmic_bytes(lowered, batch, refs)
-    # every surviving C3 instance is k = 1 (M = 64 <= 64): the fast-path kernel moves alg_solve; the
-    # general kernel only scans the verdict bytes (no instance is routed to it)
+    # every surviving C3 instance is k = 1 (M = 64 <= 64): the k = 1 kernel moves the solve bytes;
+    # the general kernel only scans the verdict bytes (no C3 instance is routed to it)
     alg = {"halda_screen_kernel": alg_screen, "halda_solve_k1_kernel": alg_solve,
            "halda_solve_kernel": batch.n_inst}[dom]
     solve_ms = phase_ms[dom]

@@ -39,8 +39,6 @@
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kRows = 4;            // capacity rows per device (link, RAM/Metal cap, <= 2 VRAM)
 constexpr int kMaxRowNnz = 8;       // widest HALDA row (cycle rows: 6 device cols + z + C)
 constexpr double kSlackEps = 1e-9;  // a capacity row counts as met within 1e-9 layers (oracle: same)
@@ -131,11 +129,14 @@ __device__ inline int64_t shfl64(int64_t v, int src) {
     return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
 }
 
-__global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls,
-                                                                int mmax, int r1max, int tab, int tab_kc) {
-    const int lane = threadIdx.x & 63;
-    const int64_t i0 = (int64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6)) * kScreenPer;
-    if (i0 >= B.n_inst) return;
+// Per-lane outcome of screen_group: lane g < kScreenPer describes instance i0 + g.
+struct ScreenOut {
+    int N, m, verdict;
+    int64_t co, ro, cs;
+};
+
+__device__ inline void screen_group(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i0, int lane,
+                                    int mmax, int r1max, int tab, int tab_kc, ScreenOut &so) {
     // lane g < kScreenPer: header of instance i0 + g
     const int64_t my = i0 + lane;
     const bool own = lane < kScreenPer && my < B.n_inst;
@@ -214,6 +215,12 @@ __global__ __launch_bounds__(kBlock) void halda_screen_kernel(halda_batch B, hal
             verdict = v;
         }
     }
+    so.N = N;
+    so.m = m;
+    so.co = co;
+    so.ro = ro;
+    so.cs = cs;
+    so.verdict = own ? verdict : CLS_DONE;
     if (own) {
         cls[my] = uint8_t(verdict);
         if (verdict == CLS_DONE) {
@@ -1236,6 +1243,83 @@ __device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &round
 #define HALDA_K1_WAVES_PER_SIMD 4  // occupancy target of the k = 1 kernel (register budget)
 #endif
 
+// One k = 1 instance (lane = device) from decode to x; hands the instance to the
+// general kernel (cls = CLS_GEN) when the fast path does not apply.
+__device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w, const Inst &I,
+                         int lane) {
+    HALDA_STAMP(0);
+    int bad = 0;
+    const int sumlo = device_pass(B, w, I, lane, bad);
+    wave_sync();
+    HALDA_STAMP(1);
+    bad |= row_pass(B, w, I, lane);
+    wave_sync();
+    HALDA_STAMP(2);
+    bad |= check_rows(w, I.M, lane);
+    if (wave_or(bad)) {
+        if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
+        return;
+    }
+    HALDA_STAMP(3);
+    Dev d = {};
+    if (lane < I.M) load_dev(d, B, w, I.co, I.M, lane, I.Wd);
+    HALDA_STAMP(4);
+    int e = 0, rounds = 0;
+    const int rc = k1_alloc(d, I.M, I.W - sumlo, lane, e, rounds);
+    wave_sync();  // LDS records are rewritten by the next instance
+    HALDA_STAMP(5);
+    if (rc == K1_FALLBACK) {
+        if (lane == 0) cls[I.inst] = CLS_GEN;  // the general kernel (launched next) takes it
+        return;
+    }
+    if (rc == K1_INFEASIBLE) {
+        if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_INFEASIBLE, 1);
+        return;
+    }
+    double g = 0.0, H = 0.0;
+    if (lane < I.M) {
+        const int wl = d.wlo + e;
+        double P, Q;
+        int n = 0, s[4] = {0, 0, 0, 0};
+        split_full(d, wl, g, n, s);
+        dev_cycle(d, wl, n, s, P, Q);
+        double *x = Rz.x + I.co;
+        const int M = I.M;
+        x[lane] = double(wl);
+        x[M + lane] = double(n);
+        x[2 * M + lane] = double(s[0]);
+        x[3 * M + lane] = double(s[1]);
+        x[4 * M + lane] = double(s[2]);
+        x[5 * M + lane] = double(s[3]);
+        x[6 * M + lane] = Q > P ? 0.5 * (Q - P) : 0.0;
+        H = Q >= P ? 0.5 * (P + Q) : P;
+    }
+    const double hmax = fmax(0.0, wave_max(lane < I.M ? H : 0.0));
+    const double gsum = wave_sum_f64(lane < I.M ? g : 0.0);
+    if (lane == 0) {
+        const double obj = gsum + I.kc * hmax;
+        Rz.x[I.co + I.iC] = hmax;
+        Rz.status[I.inst] = HALDA_STATUS_OPTIMAL;
+        Rz.obj_lin[I.inst] = obj;
+        Rz.dual_bound[I.inst] = obj;
+        Rz.gap[I.inst] = 0.0;
+        Rz.nodes[I.inst] = rounds;
+    }
+    HALDA_STAMP(6);
+}
+
+// Screen: four waves per workgroup, each screening kScreenPer consecutive instances.
+__global__ __launch_bounds__(256) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls, int mmax,
+                                                           int r1max, int tab, int tab_kc) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i0 = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kScreenPer;
+    if (i0 >= B.n_inst) return;
+    ScreenOut so;
+    screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so);
+}
+
+// k = 1 fast path: persistent 64-thread workgroups (one wave each) over the
+// instances the screen classed CLS_K1; wave b owns instances b + j * gridDim.x.
 __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_kernel(halda_batch B, halda_result Rz,
                                                                                       uint8_t *cls, int mmax) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1266,65 +1350,7 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
             I.Wd = B.row_ub[I.ro + I.m - 1];
             I.W = int(I.Wd);
             I.kc = B.c[I.co + I.iC];
-            HALDA_STAMP(0);
-            int bad = 0;
-            const int sumlo = device_pass(B, w, I, lane, bad);
-            wave_sync();
-            HALDA_STAMP(1);
-            bad |= row_pass(B, w, I, lane);
-            wave_sync();
-            HALDA_STAMP(2);
-            bad |= check_rows(w, I.M, lane);
-            if (wave_or(bad)) {
-                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
-                continue;
-            }
-            HALDA_STAMP(3);
-            Dev d = {};
-            if (lane < I.M) load_dev(d, B, w, I.co, I.M, lane, I.Wd);
-            HALDA_STAMP(4);
-            int e = 0, rounds = 0;
-            const int rc = k1_alloc(d, I.M, I.W - sumlo, lane, e, rounds);
-            wave_sync();  // LDS records are rewritten by the next instance
-            HALDA_STAMP(5);
-            if (rc == K1_FALLBACK) {
-                if (lane == 0) cls[I.inst] = CLS_GEN;
-                continue;
-            }
-            if (rc == K1_INFEASIBLE) {
-                if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_INFEASIBLE, 1);
-                continue;
-            }
-            double g = 0.0, H = 0.0;
-            if (lane < I.M) {
-                const int wl = d.wlo + e;
-                double P, Q;
-                int n = 0, s[4] = {0, 0, 0, 0};
-                split_full(d, wl, g, n, s);
-                dev_cycle(d, wl, n, s, P, Q);
-                double *x = Rz.x + I.co;
-                const int M = I.M;
-                x[lane] = double(wl);
-                x[M + lane] = double(n);
-                x[2 * M + lane] = double(s[0]);
-                x[3 * M + lane] = double(s[1]);
-                x[4 * M + lane] = double(s[2]);
-                x[5 * M + lane] = double(s[3]);
-                x[6 * M + lane] = Q > P ? 0.5 * (Q - P) : 0.0;
-                H = Q >= P ? 0.5 * (P + Q) : P;
-            }
-            const double hmax = fmax(0.0, wave_max(lane < I.M ? H : 0.0));
-            const double gsum = wave_sum_f64(lane < I.M ? g : 0.0);
-            if (lane == 0) {
-                const double obj = gsum + I.kc * hmax;
-                Rz.x[I.co + I.iC] = hmax;
-                Rz.status[I.inst] = HALDA_STATUS_OPTIMAL;
-                Rz.obj_lin[I.inst] = obj;
-                Rz.dual_bound[I.inst] = obj;
-                Rz.gap[I.inst] = 0.0;
-                Rz.nodes[I.inst] = rounds;
-            }
-            HALDA_STAMP(6);
+            solve_k1(B, Rz, cls, w, I, lane);
         }
     }
 }
@@ -1347,12 +1373,36 @@ struct Ctx {
     int device = 0;
     int cus = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after screen, after k=1 kernel
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
     void *scratch = nullptr;  // host-API staging
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
     size_t work_bytes = 0;
+    // resident workgroups per CU by (kernel, dynamic LDS), raising the LDS limit once per size
+    struct Occ {
+        const void *fn;
+        int64_t lds;
+        int per_cu;
+    } occ[8] = {};
+    int n_occ = 0;
+    hipError_t occupancy(const void *fn, int64_t lds, int *per_cu) {
+        for (int i = 0; i < n_occ; ++i)
+            if (occ[i].fn == fn && occ[i].lds == lds) {
+                *per_cu = occ[i].per_cu;
+                return hipSuccess;
+            }
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        int p = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, fn, 64, size_t(lds));
+        if (e != hipSuccess) return e;
+        p = std::max(1, p);
+        occ[n_occ % 8] = Occ{fn, lds, p};
+        n_occ = std::min(n_occ + 1, 8);
+        *per_cu = p;
+        return hipSuccess;
+    }
 };
 
 int64_t slice_bytes_for(int mmax, int r1max, int tab, int tab_kc) {
@@ -1384,32 +1434,33 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     uint8_t *cls = static_cast<uint8_t *>(ctx->work);
     HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
-    hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
-                       stream, in, out, cls, mmax, in.max_R1, int(tab), int(tab_kc));
+    hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out, cls,
+                       mmax, in.max_R1, int(tab), int(tab_kc));
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->evs, stream));
-    // k = 1 fast path: small LDS slice (device records only), high occupancy
+    HIP_TRY(hipEventRecord(ctx->evk, stream));
+    // k = 1 fast path: small LDS slice (device records only), persistent grid = resident capacity
     {
         const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
         int per_cu = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, halda_solve_k1_kernel, 64, size_t(lds1)));
-        per_cu = std::max(1, per_cu);
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_kernel), lds1, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
         hipLaunchKernelGGL(halda_solve_k1_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls, mmax);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ctx->evk, stream));
-    // general kernel: k > 1, fleets wider than 64, and k = 1 instances the fast path handed over
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(halda_solve_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-    // persistent grid: exactly the resident capacity (one 64-thread workgroup = one wave)
-    int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, halda_solve_kernel, 64, size_t(lds)));
-    per_cu = std::max(1, per_cu);
-    const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
-    hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds), stream, in, out, cls, mmax,
-                       in.max_R1, int(tab), int(tab_kc));
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->evs, stream));
+    // general kernel: k > 1, fleets wider than kK1MaxM devices, and the k = 1 instances the fast path
+    // handed back (rare). Persistent grid = the resident capacity when the batch's shape summary
+    // admits k > 1 or wide instances; otherwise only hand-backs can reach it: one wave per CU.
+    {
+        int per_cu = 0;
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds, &per_cu));
+        const bool general_work = in.max_tab_kc > 0 || (in.max_cols - 1) / 7 > kK1MaxM;
+        const int64_t cap = general_work ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(cap, in.n_inst)));
+        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds), stream, in, out, cls, mmax,
+                           in.max_R1, int(tab), int(tab_kc));
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
     return HALDA_OK;
@@ -1509,9 +1560,9 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
     if (!c->timed) return fail(HALDA_E_ARG, "no solve has been launched on this context");
     HIP_TRY(hipEventSynchronize(c->ev1));
     float a = 0.f, b = 0.f, d = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evs));
-    HIP_TRY(hipEventElapsedTime(&b, c->evs, c->evk));
-    HIP_TRY(hipEventElapsedTime(&d, c->evk, c->ev1));
+    HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evk));
+    HIP_TRY(hipEventElapsedTime(&b, c->evk, c->evs));
+    HIP_TRY(hipEventElapsedTime(&d, c->evs, c->ev1));
     ms3[0] = a;
     ms3[1] = b;
     ms3[2] = d;

@@ -113,14 +113,14 @@ int halda_solve_batch(void *ctx, const halda_batch *in, halda_result *out);
  * enqueued on `stream` (a hipStream_t; NULL = the context's stream). */
 int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out, void *stream);
 
-/* Device time of the last solve's kernel sequence (screen + compact + solve) in ms. */
+/* Device time of the last solve's kernel sequence (both launches) in ms. */
 int halda_last_kernel_ms(void *ctx, double *ms);
 
-/* Device time of the last solve's solve kernels (k = 1 fast path + general), in ms. */
+/* Device time of the last solve's general kernel (halda_solve_kernel) alone, in ms. */
 int halda_last_solve_kernel_ms(void *ctx, double *ms);
 
-/* Device time of the last solve per launch, in ms: ms3[0] screen kernel,
- * ms3[1] k = 1 fast-path kernel, ms3[2] general solve kernel. */
+/* Device time of the last solve per launch, in ms: ms3[0] the screen kernel,
+ * ms3[1] the k = 1 fast-path kernel, ms3[2] the general kernel. */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */

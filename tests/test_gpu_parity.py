@@ -185,3 +185,35 @@ def test_host_api_computes_shape_summary_itself(llama_online_model):
     a = get_context(0).solve(batch)
     b = get_context(0).solve(auto)
     assert np.array_equal(a.status, b.status) and np.array_equal(a.x, b.x)
+
+
+@pytest.mark.parametrize("M,seed", [(6, 3), (16, 1), (64, 2)])
+def test_k1_hand_back_path(llama_online_model, M, seed):
+    """A k = 1 leaf that does not start at w = lb(w) (here lb(n_i) = 3 with n_i <= w_i, so w_i >= 3):
+    the fast path hands the instance to the general path (tables in global scratch). GPU == exact
+    oracle on the same modified MILP."""
+    from distilp_amd.common import DeviceProfile
+
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(seed, M)]
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    batch, refs = assemble([fl], [[1]])
+    p = mo.lower_dense(devs, llama_online_model, 1, 0.5)
+    gpu_dev = [i for i in range(M) if p["ub"][M + i] > 0]
+    assert gpu_dev, "fleet needs a device with a GPU split"
+    i = gpu_dev[0]
+    batch.col_lb = batch.col_lb.copy()
+    batch.col_lb[refs[0].col_off + M + i] = 3.0
+    p["lb"] = p["lb"].copy()
+    p["lb"][M + i] = 3.0
+    res = get_context(0).solve(batch)
+    st, xo, b1, b2, _ = mo.exact_solve(p)
+    if st == 2:
+        assert res.status[0] == STATUS_INFEASIBLE
+        return
+    assert res.status[0] == STATUS_OPTIMAL
+    x = res.x[:refs[0].n_cols]
+    assert x[M + i] >= 3.0 and x[i] >= 3.0
+    assert _obj_close(float(res.obj_lin[0]), b1)
+    assert _obj_close(float(np.dot(p["c"], x)), b1)
+    if mo.uniqueness_margin_ok(b1, b2):
+        assert np.array_equal(x[:2 * M], xo[:2 * M])
