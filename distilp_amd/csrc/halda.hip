@@ -743,59 +743,55 @@ __device__ inline int block_of(int j, int M, float invM) {
     return q;
 }
 
-// Classify one CSR row by its nonzero pattern and record it for its device.
-// Returns nonzero when the row does not fit the HALDA structure.
-__device__ inline int decode_row(const WaveCtx &w, const Inst &I, int nnz, double rhs, double rlb,
-                                 const int (&cols)[kMaxRowNnz], const double (&vals)[kMaxRowNnz]) {
+// Cycle row of one device (its last entry is C): busy(i) +- z_i - C <= rhs,
+// whose non-w part must equal the device's objective entries. Records the w
+// coefficient and rhs. Returns nonzero when the row does not fit.
+template <int NZ>
+__device__ inline int decode_cycle_row(const WaveCtx &w, const Inst &I, int nnz, double rhs, double vlast, int zc,
+                                       double vz, const int (&cols)[NZ], const double (&vals)[NZ]) {
     const int M = I.M;
-    if (rlb != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs) < 1e300)) return 1;
-    int last = -1, zc = -1;
-    double vlast = 0.0, vz = 0.0;
+    const int dev = zc - 6 * M;
+    if (vlast != -1.0 || nnz < 2 || dev < 0 || dev >= M || fabs(vz) != 1.0) return 1;
+    const double *cst = w.cost + 6 * dev;
+    double coef0 = 0.0;
+    int seen = 0, rb = 0;  // seen: bitmask of blocks present
 #pragma unroll
-    for (int k = 0; k < kMaxRowNnz; ++k) {
-        if (k == nnz - 1) { last = cols[k]; vlast = vals[k]; }
-        if (k == nnz - 2) { zc = cols[k]; vz = vals[k]; }
-    }
-    int rb = 0;
-    if (last == I.iC) {
-        // cycle row: busy(i) +- z_i - C <= rhs; its non-w part must equal the objective's
-        const int dev = zc - 6 * M;
-        if (vlast != -1.0 || nnz < 2 || dev < 0 || dev >= M || fabs(vz) != 1.0) return 1;
-        const double *cst = w.cost + 6 * dev;
-        double coef0 = 0.0;
-        int seen = 0;  // bitmask of blocks present
-#pragma unroll
-        for (int k = 0; k < kMaxRowNnz; ++k) {
-            if (k < nnz - 2) {
-                const int j = cols[k];
-                const int blk = block_of(j, M, I.invM);
-                if (j >= 6 * M || j - blk * M != dev) rb = 1;
-                else if (blk == 0) coef0 = vals[k];
-                else {
-                    rb |= vals[k] != cst[blk];
-                    seen |= 1 << blk;
-                }
+    for (int k = 0; k < NZ; ++k) {
+        if (k < nnz - 2) {
+            const int j = cols[k];
+            const int blk = block_of(j, M, I.invM);
+            if (j >= 6 * M || j - blk * M != dev) rb = 1;
+            else if (blk == 0) coef0 = vals[k];
+            else {
+                rb |= vals[k] != cst[blk];
+                seen |= 1 << blk;
             }
         }
-        // absent entries must be zero in the objective too
-#pragma unroll
-        for (int b = 1; b < 6; ++b) rb |= !((seen >> b) & 1) && cst[b] != 0.0;
-        if (!rb) {
-            const bool first = vz > 0.0;
-            w.cyc[4 * dev + (first ? 0 : 1)] = coef0;
-            w.cyc[4 * dev + (first ? 2 : 3)] = rhs;
-            atomicAdd(&w.cnt[dev], first ? (1 << 8) : (1 << 16));
-        }
-        return rb;
     }
-    // capacity / link row of one device: aw w + an n - beta s <= rhs
-    int dev = -1, slack = -1;
+    // absent entries must be zero in the objective too
+#pragma unroll
+    for (int b = 1; b < 6; ++b) rb |= !((seen >> b) & 1) && cst[b] != 0.0;
+    if (!rb) {
+        const bool first = vz > 0.0;
+        w.cyc[4 * dev + (first ? 0 : 1)] = coef0;
+        w.cyc[4 * dev + (first ? 2 : 3)] = rhs;
+        atomicAdd(&w.cnt[dev], first ? (1 << 8) : (1 << 16));
+    }
+    return rb;
+}
+
+// Capacity / link row of one device: aw w + an n - beta s <= rhs (at most one
+// slack column). Records (slack, u, v, K). Returns nonzero when it does not fit.
+template <int NZ>
+__device__ inline int decode_cap_row(const WaveCtx &w, const Inst &I, int nnz, double rhs, const int (&cols)[NZ],
+                                     const double (&vals)[NZ]) {
+    int dev = -1, slack = -1, rb = 0;
     double aw = 0.0, an = 0.0, beta = 0.0;
 #pragma unroll
-    for (int k = 0; k < kMaxRowNnz; ++k) {
+    for (int k = 0; k < NZ; ++k) {
         if (k < nnz) {
-            const int j = cols[k], blk = block_of(j, M, I.invM), i = j - blk * M;
-            if (j >= 6 * M || (dev >= 0 && i != dev)) rb = 1;
+            const int j = cols[k], blk = block_of(j, I.M, I.invM), i = j - blk * I.M;
+            if (j >= 6 * I.M || (dev >= 0 && i != dev)) rb = 1;
             dev = i;
             if (blk == 0) aw = vals[k];
             else if (blk == 1) an = vals[k];
@@ -816,6 +812,22 @@ __device__ inline int decode_row(const WaveCtx &w, const Inst &I, int nnz, doubl
     if (q >= kRows) return 1;
     w.rows[dev * kRows + q] = make_int2((slack + 1) | ((u + 1) << 8) | ((v + 1) << 16), int(kk));
     return 0;
+}
+
+// Classify one CSR row by its nonzero pattern and record it for its device.
+// Returns nonzero when the row does not fit the HALDA structure.
+__device__ inline int decode_row(const WaveCtx &w, const Inst &I, int nnz, double rhs, double rlb,
+                                 const int (&cols)[kMaxRowNnz], const double (&vals)[kMaxRowNnz]) {
+    if (rlb != -kInf || nnz < 1 || nnz > kMaxRowNnz || !(fabs(rhs) < 1e300)) return 1;
+    int last = -1, zc = -1;
+    double vlast = 0.0, vz = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxRowNnz; ++k) {
+        if (k == nnz - 1) { last = cols[k]; vlast = vals[k]; }
+        if (k == nnz - 2) { zc = cols[k]; vz = vals[k]; }
+    }
+    if (last == I.iC) return decode_cycle_row<kMaxRowNnz>(w, I, nnz, rhs, vlast, zc, vz, cols, vals);
+    return decode_cap_row<kMaxRowNnz>(w, I, nnz, rhs, cols, vals);
 }
 
 // Row pass: lane-strided rows, two rows per lane per step; the next step's row
@@ -862,6 +874,11 @@ __device__ int row_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, i
     }
     return bad;
 }
+
+// Capacity-row staging of the k = 1 decode (decode_k1).
+constexpr int kCapNnz = 3;     // widest capacity / link row (w, n, one slack)
+constexpr int kCapSlots = 4;   // capacity rows per lane: up to 256 rows
+constexpr int kCycSlots = 2;   // cycle rows per lane: 2M <= 128
 
 // Per device: one row of each cycle kind, <= 2 pure rows, and the rows of one
 // slack share their (u, v) pattern.
@@ -1021,6 +1038,14 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
     do {               \
     } while (0)
 #endif
+// -DHALDA_STAMPS_DECODE: stamps 1..5 mark the round trips inside decode_k1 instead
+#ifdef HALDA_STAMPS_DECODE
+#define HALDA_DSTAMP(k) HALDA_STAMP(k)
+#define HALDA_PSTAMP(k) do {} while (0)
+#else
+#define HALDA_DSTAMP(k) do {} while (0)
+#define HALDA_PSTAMP(k) HALDA_STAMP(k)
+#endif
 
 #ifndef HALDA_SOLVE_WAVES_PER_SIMD
 #define HALDA_SOLVE_WAVES_PER_SIMD 2  // occupancy target of the solve kernel (register budget)
@@ -1114,17 +1139,28 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
 // leaf_ranges); an instance whose leaves do not start at e = 0 or fail the
 // check is handed to the general kernel (cls = CLS_GEN), never approximated.
 
+// LDS slice of one k = 1 wave: capacity-row records, per-device row counters
+// and a staging buffer for one coalesced CSR segment (kStage entries: col_idx
+// then val). The generic decode (hand-back of a CSR in another row order) keeps
+// its cyc / cost records in the staging buffer instead.
+constexpr int kStage = 512;
+constexpr int kStageColBytes = kStage * 4 + 32;  // 16-B chunks from the segment start rounded down
+constexpr int kStageValBytes = kStage * 8 + 32;
+
 struct K1Slice {
-    int64_t rows, cyc, cost, cnt, total;
+    int64_t rows, cnt, stage, cyc, cost, total;
 };
 
 __host__ __device__ inline K1Slice make_k1_slice(int mmax) {
     K1Slice s;
     int64_t o = 0;
-    s.rows = o; o = align16(o + int64_t(mmax) * kRows * 8);
-    s.cyc = o;  o = align16(o + int64_t(mmax) * 4 * 8);
-    s.cost = o; o = align16(o + int64_t(mmax) * 6 * 8);
-    s.cnt = o;  o = align16(o + int64_t(mmax) * 4);
+    s.rows = o;  o = align16(o + int64_t(mmax) * kRows * 8);
+    s.cnt = o;   o = align16(o + int64_t(mmax) * 4);
+    s.stage = o;
+    const int64_t st = kStageColBytes + kStageValBytes, rec = int64_t(mmax) * (4 + 6) * 8;
+    o = align16(o + (st > rec ? st : rec));
+    s.cyc = s.stage;
+    s.cost = s.stage + int64_t(mmax) * 4 * 8;
     s.total = o;
     return s;
 }
@@ -1243,31 +1279,307 @@ __device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &round
 #define HALDA_K1_WAVES_PER_SIMD 4  // occupancy target of the k = 1 kernel (register budget)
 #endif
 
+// LDS-DMA staging (global_load_lds_dwordx4): bytes [p, p + nbytes) land in dst
+// as lane-linear 16-B chunks from p rounded down to 16 B (each wave
+// instruction fills 1 KiB); returns p's byte offset in dst. No VGPR holds the
+// data; stage_wait() retires the copies before the LDS is read. Chunks may read
+// up to 15 B past the range (the caller guarantees they are in the array).
+__device__ inline void glds16(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+
+__device__ inline int stage_lds(const void *p, int nbytes, unsigned char *dst, int lane) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p), a0 = a & ~uintptr_t(15);
+    const int chunks = int((a + uintptr_t(nbytes) - a0 + 15) >> 4);
+    for (int c0 = 0; c0 < chunks; c0 += 64)
+        if (c0 + lane < chunks) glds16(reinterpret_cast<const void *>(a0 + 16 * uintptr_t(c0 + lane)), dst + 16 * c0);
+    return int(a - a0);
+}
+
+__device__ inline void stage_wait() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+}
+
+__device__ inline double shfl_f64(double v, int src) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __shfl(int(uint32_t(u)), src), hi = __shfl(int(uint32_t(u >> 32)), src);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+
+constexpr int kRpSlots = 5;  // row pointers rp[0 .. ncap] per lane: ncap <= 64 * 5 - 1
+
+// Staged decode of one k = 1 instance (M <= 64, lane = device), for a CSR in
+// the reference's row order (capacity / link / VRAM rows, then the two cycle
+// rows of each device in device order, then the equality row;
+// halda_p_solver.py:177-297). Every CSR segment is read with coalesced loads
+// into the LDS staging buffer and decoded from there (lane-strided gathers
+// straight from HBM touch one cache line per lane and entry):
+//   round trip 1  this lane's device columns (c, bounds, integrality) and the
+//                 capacity rows' pointers and bounds;
+//   round trip 2  the capacity segment's entries, the cycle rows' pointers and bounds;
+//   round trip 3  the cycle segment's entries (two halves of <= 64 rows).
+// Capacity rows go through decode_cap_row (LDS records, as the generic path);
+// the cycle rows of device i are decoded by lanes 2i, 2i + 1 (mod 64) against
+// device i's objective entries (shuffled from lane i) and land in lane i's
+// registers. Fills d. Returns 0 ok, 1 not a HALDA MILP, 2 not in this shape
+// (the caller then runs the generic decode).
+__device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *scol_raw, unsigned char *sval_raw,
+                         const Inst &I, int lane, Dev &d, int &sumlo) {
+    const int M = I.M, ncyc = 2 * M, ncap = I.m - 1 - ncyc;
+    // M >= 4: the staged 16-B chunks past a segment's end stay inside the equality row
+    if (M < 4 || ncap < 0 || ncap > 64 * kCapSlots || ncyc > 64 * kCycSlots) return 2;
+    const bool act = lane < M;
+    const int64_t co = I.co;
+    // ---- round trip 1 (branch-free: out-of-range lanes read a valid element and
+    // discard it, so the compiler issues every load before the first wait)
+    const int li = act ? lane : 0;
+    double cv[6], lbv[6], ubv[6];
+    uint8_t ig[6];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        cv[b] = B.c[co + b * M + li];
+        lbv[b] = B.col_lb[co + b * M + li];
+        ubv[b] = B.col_ub[co + b * M + li];
+        ig[b] = B.integrality[co + b * M + li];
+    }
+    const double cz = B.c[co + 6 * M + li], lz = B.col_lb[co + 6 * M + li], uz = B.col_ub[co + 6 * M + li];
+    const uint8_t iz = B.integrality[co + 6 * M + li];
+    const uint8_t iC = B.integrality[co + I.iC];
+    const double lC = B.col_lb[co + I.iC], uC = B.col_ub[co + I.iC];
+    int rpv[kRpSlots];
+    double rub[kCapSlots], rlb[kCapSlots];
+#pragma unroll
+    for (int j = 0; j < kRpSlots; ++j) rpv[j] = I.rp[min(lane + 64 * j, ncap)];
+#pragma unroll
+    for (int j = 0; j < kCapSlots; ++j) {
+        const int r = min(lane + 64 * j, I.m - 1);
+        rub[j] = B.row_ub[I.ro + r];
+        rlb[j] = B.row_lb[I.ro + r];
+    }
+    const int cbase = I.rp[0], cend = I.rp[ncap];
+    int dbad = iz != 0 || cz != 0.0 || lz != 0.0 || uz != kInf || lbv[1] < 0.0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) dbad |= ig[b] != 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dbad |= !(cv[2 + j] >= 0.0);
+    int bad = act ? dbad : 0;
+    const int lo = act ? int(ceil(lbv[0])) : 0;
+    if (act) w.cnt[lane] = 0;
+    bad |= !(I.kc >= 0.0) || iC != 0 || lC != 0.0 || uC != kInf;
+    sumlo = wave_sum(lo);
+    HALDA_DSTAMP(1);
+    d.cw = cv[0]; d.cn = cv[1]; d.cs0 = cv[2]; d.cs1 = cv[3]; d.cs2 = cv[4]; d.cs3 = cv[5];
+    d.wlo = int(ceil(lbv[0]));
+    d.whi = int(floor(fmin(ubv[0], I.Wd)));
+    d.nlo = int(ceil(lbv[1]));
+    d.nhi = int(floor(fmin(ubv[1], I.Wd)));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        d.slo[j] = int(ceil(lbv[2 + j]));
+        d.shi[j] = int(floor(fmin(ubv[2 + j], 1e6)));
+        d.us[j] = d.vs[j] = 0;
+        d.Ks[j] = kNoRow;
+    }
+    d.uf[0] = d.vf[0] = d.uf[1] = d.vf[1] = 0;
+    d.Kf[0] = d.Kf[1] = 0;
+    d.r1w = d.r2w = d.rhs1 = d.rhs2 = 0.0;
+
+    // ---- round trip 2: capacity entries (LDS-DMA, coalesced), cycle row pointers / bounds
+    const int nc = cend - cbase;
+    if (nc < 0 || nc > kStage) return 2;
+    const int *scol = reinterpret_cast<const int *>(scol_raw) + stage_lds(B.col_idx + cbase, 4 * nc, scol_raw, lane) / 4;
+    const double *sval =
+        reinterpret_cast<const double *>(sval_raw) + stage_lds(B.val + cbase, 8 * nc, sval_raw, lane) / 8;
+    int yrs[kCycSlots], yre[kCycSlots];
+    double yub[kCycSlots], ylb[kCycSlots];
+#pragma unroll
+    for (int h = 0; h < kCycSlots; ++h) {
+        const int r = min(ncap + 64 * h + lane, ncap + ncyc - 1);
+        yrs[h] = I.rp[r];
+        yre[h] = I.rp[r + 1];
+        yub[h] = B.row_ub[I.ro + r];
+        ylb[h] = B.row_lb[I.ro + r];
+    }
+    int hb[kCycSlots], he[kCycSlots];
+#pragma unroll
+    for (int h = 0; h < kCycSlots; ++h) {
+        hb[h] = I.rp[min(ncap + 64 * h, ncap + ncyc)];
+        he[h] = I.rp[min(ncap + 64 * h + 64, ncap + ncyc)];
+    }
+    // row ends of the capacity rows: rp[r + 1] from the next lane (slot j + 1 for lane 63)
+    int rpe[kCapSlots];
+#pragma unroll
+    for (int j = 0; j < kCapSlots; ++j) {
+        const int nx = __shfl(rpv[j], (lane + 1) & 63), wrap = __shfl(rpv[j + 1], 0);
+        rpe[j] = lane == 63 ? wrap : nx;
+    }
+    stage_wait();  // staged entries and zeroed counters visible
+    HALDA_DSTAMP(2);
+#pragma unroll
+    for (int j = 0; j < kCapSlots; ++j) {
+        const int r = lane + 64 * j;
+        if (r < ncap) {
+            const int rs = rpv[j] - cbase, nz = rpe[j] - rpv[j];
+            if (nz < 1 || rs < 0 || rs + nz > nc) {
+                bad |= 1;
+            } else if (scol[rs + nz - 1] == I.iC) {
+                bad |= 2;  // a cycle row among the capacity rows: another row order
+            } else if (rlb[j] != -kInf || nz > kCapNnz || !(fabs(rub[j]) < 1e300)) {
+                bad |= 1;
+            } else {
+                int cols[kCapNnz];
+                double vals[kCapNnz];
+#pragma unroll
+                for (int k = 0; k < kCapNnz; ++k) {
+                    cols[k] = k < nz ? scol[rs + k] : -1;
+                    vals[k] = k < nz ? sval[rs + k] : 0.0;
+                }
+                bad |= decode_cap_row<kCapNnz>(w, I, nz, rub[j], cols, vals);
+            }
+        }
+    }
+
+    HALDA_DSTAMP(3);
+    // ---- round trip 3 (and 4): cycle segment, two halves of <= 64 rows (32 devices each)
+#pragma unroll
+    for (int h = 0; h < kCycSlots; ++h) {
+        const int rows = min(64, ncyc - 64 * h);
+        if (rows <= 0) break;
+        const int hn = he[h] - hb[h];
+        if (hn < 0 || hn > kStage) return 2;
+        wave_sync();  // the previous segment's readers are done
+        scol = reinterpret_cast<const int *>(scol_raw) + stage_lds(B.col_idx + hb[h], 4 * hn, scol_raw, lane) / 4;
+        sval = reinterpret_cast<const double *>(sval_raw) + stage_lds(B.val + hb[h], 8 * hn, sval_raw, lane) / 8;
+        stage_wait();
+        if (h == 0) HALDA_DSTAMP(4);
+        else HALDA_DSTAMP(5);
+        // lane l: row ncap + 64 h + l = cycle row (l & 1) of device 32 h + l / 2
+        const int want = 32 * h + (lane >> 1);
+        int dev = 0, rb = 0, shape = 0;
+        double coef0 = 0.0;
+        const bool mine = lane < rows;
+        const int rs = yrs[h] - hb[h], nz = yre[h] - yrs[h];
+        if (mine) {
+            if (nz < 2 || rs < 0 || rs + nz > hn) {
+                rb = 1;
+            } else {
+                const int last = scol[rs + nz - 1];
+                const double vlast = sval[rs + nz - 1];
+                const int zc = scol[rs + nz - 2];
+                const double vz = sval[rs + nz - 2];
+                dev = zc - 6 * M;
+                if (last != I.iC) shape = 1;  // a capacity row among the cycle rows
+                else if (ylb[h] != -kInf || nz > kMaxRowNnz || !(fabs(yub[h]) < 1e300) || vlast != -1.0 ||
+                         dev < 0 || dev >= M || fabs(vz) != 1.0)
+                    rb = 1;
+                else if (dev != want || (vz > 0.0) != ((lane & 1) == 0))
+                    shape = 1;  // valid cycle row, another order
+            }
+        }
+        // the device's objective entries (blocks 1..5) from lane dev
+        const bool ok = mine && !rb && !shape;
+        const int src = ok ? dev : 0;
+        double cst[6];
+        cst[0] = 0.0;
+        cst[1] = shfl_f64(d.cn, src);
+        cst[2] = shfl_f64(d.cs0, src);
+        cst[3] = shfl_f64(d.cs1, src);
+        cst[4] = shfl_f64(d.cs2, src);
+        cst[5] = shfl_f64(d.cs3, src);
+        if (ok) {
+            int seen = 0;
+            for (int k = 0; k < nz - 2; ++k) {
+                const int j = scol[rs + k];
+                const double v = sval[rs + k];
+                const int blk = block_of(j, M, I.invM);
+                if (j >= 6 * M || j - blk * M != dev) rb = 1;
+                else if (blk == 0) coef0 = v;
+                else {
+                    double cb = cst[1];
+#pragma unroll
+                    for (int b = 2; b < 6; ++b)
+                        if (blk == b) cb = cst[b];
+                    rb |= v != cb || ((seen >> blk) & 1);
+                    seen |= 1 << blk;
+                }
+            }
+#pragma unroll
+            for (int b = 1; b < 6; ++b) rb |= !((seen >> b) & 1) && cst[b] != 0.0;
+        }
+        bad |= rb | (shape << 1);
+        // device i (lanes 32 h .. 32 h + 31) takes rows 2 (i - 32 h) and 2 (i - 32 h) + 1
+        const int s0 = (2 * (lane - 32 * h)) & 63, s1 = (s0 + 1) & 63;
+        const double c0 = shfl_f64(coef0, s0), c1 = shfl_f64(coef0, s1);
+        const double h0 = shfl_f64(yub[h], s0), h1 = shfl_f64(yub[h], s1);
+        if (act && lane >= 32 * h && lane < 32 * h + 32) {
+            d.r1w = c0;
+            d.rhs1 = h0;
+            d.r2w = c1;
+            d.rhs2 = h1;
+        }
+    }
+    bad = wave_or(bad);
+    if (bad) return (bad & 2) ? 2 : 1;
+    wave_sync();  // capacity records complete
+    // capacity records -> this lane's device (load_dev / check_rows semantics)
+    if (act) {
+        const int nrow = w.cnt[lane] & 0xff;
+        if (nrow > kRows) {
+            bad = 1;
+        } else {
+            int nf = 0;
+            for (int q = 0; q < nrow; ++q) {
+                const int2 r = w.rows[lane * kRows + q];
+                const int kind = (r.x & 0xff) - 1, u = ((r.x >> 8) & 0xff) - 1, v = ((r.x >> 16) & 0xff) - 1;
+                if (kind < 0) {
+                    if (nf == 0) { d.uf[0] = u; d.vf[0] = v; d.Kf[0] = r.y; }
+                    else { d.uf[1] = u; d.vf[1] = v; d.Kf[1] = r.y; }
+                    ++nf;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (kind == j) {
+                        bad |= d.Ks[j] != kNoRow && (d.us[j] != u || d.vs[j] != v);  // one (u, v) per slack
+                        d.us[j] = u;
+                        d.vs[j] = v;
+                        d.Ks[j] = max(d.Ks[j], r.y);
+                    }
+                }
+            }
+            bad |= nf > 2;
+        }
+    }
+    return wave_or(bad);
+}
+
 // One k = 1 instance (lane = device) from decode to x; hands the instance to the
 // general kernel (cls = CLS_GEN) when the fast path does not apply.
-__device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w, const Inst &I,
-                         int lane) {
+__device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w,
+                         unsigned char *scol, unsigned char *sval, const Inst &I, int lane) {
     HALDA_STAMP(0);
-    int bad = 0;
-    const int sumlo = device_pass(B, w, I, lane, bad);
-    wave_sync();
-    HALDA_STAMP(1);
-    bad |= row_pass(B, w, I, lane);
-    wave_sync();
-    HALDA_STAMP(2);
-    bad |= check_rows(w, I.M, lane);
-    if (wave_or(bad)) {
-        if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
+    Dev d = {};
+    int sumlo = 0;
+    const int fast = decode_k1(B, w, scol, sval, I, lane, d, sumlo);
+    HALDA_PSTAMP(1);
+    if (fast == 2) {  // another row order / shape: the general kernel (generic decode) takes it
+        if (lane == 0) cls[I.inst] = CLS_GEN;
+        wave_sync();
         return;
     }
-    HALDA_STAMP(3);
-    Dev d = {};
-    if (lane < I.M) load_dev(d, B, w, I.co, I.M, lane, I.Wd);
-    HALDA_STAMP(4);
+    if (fast == 1) {
+        if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
+        wave_sync();
+        return;
+    }
+    HALDA_PSTAMP(2);
+    HALDA_PSTAMP(3);
+    HALDA_PSTAMP(4);
     int e = 0, rounds = 0;
     const int rc = k1_alloc(d, I.M, I.W - sumlo, lane, e, rounds);
     wave_sync();  // LDS records are rewritten by the next instance
-    HALDA_STAMP(5);
+    HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
         if (lane == 0) cls[I.inst] = CLS_GEN;  // the general kernel (launched next) takes it
         return;
@@ -1330,6 +1642,8 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
     w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
     w.cost = reinterpret_cast<double *>(smem + sl.cost);
     w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
+    unsigned char *scol = smem + sl.stage;
+    unsigned char *sval = smem + sl.stage + kStageColBytes;
     const int S = gridDim.x;
     for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
         const int64_t mine = base + int64_t(lane) * S;
@@ -1350,7 +1664,7 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
             I.Wd = B.row_ub[I.ro + I.m - 1];
             I.W = int(I.Wd);
             I.kc = B.c[I.co + I.iC];
-            solve_k1(B, Rz, cls, w, I, lane);
+            solve_k1(B, Rz, cls, w, scol, sval, I, lane);
         }
     }
 }

@@ -217,3 +217,36 @@ def test_k1_hand_back_path(llama_online_model, M, seed):
     assert _obj_close(float(np.dot(p["c"], x)), b1)
     if mo.uniqueness_margin_ok(b1, b2):
         assert np.array_equal(x[:2 * M], xo[:2 * M])
+
+
+@pytest.mark.parametrize("M,seed", [(5, 0), (64, 1)])
+def test_row_order_does_not_matter(llama_online_model, M, seed):
+    """The k = 1 fast path decodes rows in the reference's order (capacity rows, then cycle rows);
+    a CSR with its ub rows permuted takes the generic decode and gives the same solution."""
+    import dataclasses
+
+    from distilp_amd.common import DeviceProfile
+
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(seed, M)]
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    batch, refs = assemble([fl], [[1, 2]])
+    base = get_context(0).solve(batch)
+    m = int(batch.n_rows[0])
+    rp = batch.row_ptr[batch.csr_off[0]:batch.csr_off[0] + m + 1]
+    perm = np.random.default_rng(seed).permutation(m - 1)
+    perm = np.append(perm, m - 1)  # the equality row stays last
+    cols, vals, ptr = [], [], [0]
+    for r in perm:
+        cols.append(batch.col_idx[rp[r]:rp[r + 1]])
+        vals.append(batch.val[rp[r]:rp[r + 1]])
+        ptr.append(ptr[-1] + rp[r + 1] - rp[r])
+    row_lb, row_ub = batch.row_lb.copy(), batch.row_ub.copy()
+    for ro in batch.row_off:
+        row_lb[ro:ro + m] = batch.row_lb[ro + perm]
+        row_ub[ro:ro + m] = batch.row_ub[ro + perm]
+    shuffled = dataclasses.replace(batch, row_ptr=np.asarray(ptr, np.int32), col_idx=np.concatenate(cols),
+                                   val=np.concatenate(vals), csr_off=np.zeros_like(batch.csr_off),
+                                   row_lb=row_lb, row_ub=row_ub)
+    res = get_context(0).solve(shuffled)
+    assert np.array_equal(res.status, base.status)
+    assert np.array_equal(res.x, base.x)
