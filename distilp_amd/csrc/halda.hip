@@ -137,47 +137,63 @@ struct ScreenOut {
 
 __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i0, int lane,
                                     int mmax, int r1max, int tab, int tab_kc, ScreenOut &so) {
-    // lane g < kScreenPer: header of instance i0 + g
+    // lane g < kScreenPer: header of instance i0 + g. Loads are branch-free (lanes
+    // without an instance read a valid element and discard it) so that each round
+    // trip's loads issue before the first wait.
     const int64_t my = i0 + lane;
     const bool own = lane < kScreenPer && my < B.n_inst;
-    int N = 1, m = 1;
-    int64_t co = 0, ro = 0, cs = 0;
-    if (own) {
-        N = B.n_cols[my];
-        m = B.n_rows[my];
-        co = B.col_off[my];
-        ro = B.row_off[my];
-        cs = B.csr_off[my];
-    }
+    const int64_t mc = own ? my : i0;
+    const int N0 = B.n_cols[mc], m0 = B.n_rows[mc];
+    const int64_t co0 = B.col_off[mc], ro0 = B.row_off[mc], cs0 = B.csr_off[mc];
+    const int N = own ? N0 : 1, m = own ? m0 : 1;
+    const int64_t co = own ? co0 : 0, ro = own ? ro0 : 0, cs = own ? cs0 : 0;
     int status = 0;  // 0 = still open
     if (N < 1 || (N - 1) % 7 != 0 || m < 1) status = HALDA_STATUS_UNSUPPORTED;
     const int M = status ? 0 : (N - 1) / 7;
     if (!status && M > mmax) status = HALDA_STATUS_TOO_LARGE;
-    int eqs = 0, eqe = 0;
-    double Wd = 0.0, Wl = 0.0, cC = 0.0;
-    if (own && !status) {
-        const int32_t *rp = B.row_ptr + cs;
-        eqs = rp[m - 1];
-        eqe = rp[m];
-        Wd = B.row_ub[ro + m - 1];
-        Wl = B.row_lb[ro + m - 1];
-        cC = B.c[co + 7 * int64_t(M)];
+    // round trip 2: equality-row extent and bounds, c[C] (lane g), and the w bounds of
+    // every instance of the group (lane = device)
+    const int ma = max(m0, 1);
+    const int32_t *rp = B.row_ptr + cs0;
+    const int eqs0 = rp[ma - 1], eqe0 = rp[ma];
+    const double Wd0 = B.row_ub[ro0 + ma - 1], Wl0 = B.row_lb[ro0 + ma - 1];
+    const double cC0 = B.c[co0 + 7 * int64_t(max(M, 0))];
+    double lbv[kScreenPer], ubv[kScreenPer];
+    int Mg_[kScreenPer];
+#pragma unroll
+    for (int g = 0; g < kScreenPer; ++g) {
+        const int Mg = __shfl(M, g);
+        const int64_t cg = shfl64(co0, g);
+        const int64_t idx = cg + (lane < Mg ? lane : 0);
+        lbv[g] = B.col_lb[idx];
+        ubv[g] = B.col_ub[idx];
+        Mg_[g] = Mg;
     }
+    const bool live = own && !status;
+    const int eqs = live ? eqs0 : 0, eqe = live ? eqe0 : 0;
+    const double Wd = live ? Wd0 : 0.0, Wl = live ? Wl0 : 0.0, cC = live ? cC0 : 0.0;
     if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
         status = HALDA_STATUS_UNSUPPORTED;
 
-    // per instance g (lane = device): equality row entries and w bounds, all issued first
+    // round trip 3: equality row entries per instance g (lane = device); lanes
+    // without an entry read the first entry of an open instance's row (valid)
     int cv[kScreenPer];
-    double vv[kScreenPer], lbv[kScreenPer], ubv[kScreenPer];
+    double vv[kScreenPer];
+    const uint64_t open = __ballot(lane < kScreenPer && own && !status && M > 0);
+    const int safe = open ? __shfl(eqs0, __builtin_ctzll(open)) : 0;
 #pragma unroll
     for (int g = 0; g < kScreenPer; ++g) {
-        const int Mg = __shfl(M, g), stg = __shfl(status, g), eg = __shfl(eqs, g);
-        const int64_t cg = shfl64(co, g);
-        const bool in = i0 + g < B.n_inst && stg == 0 && lane < Mg;
-        cv[g] = in ? B.col_idx[eg + lane] : lane;
-        vv[g] = in ? B.val[eg + lane] : 1.0;
-        lbv[g] = in ? B.col_lb[cg + lane] : 0.0;
-        ubv[g] = in ? B.col_ub[cg + lane] : 0.0;
+        const int stg = __shfl(status, g), eg = __shfl(eqs0, g);
+        const bool in = open && i0 + g < B.n_inst && stg == 0 && lane < Mg_[g];
+        const int idx = in ? eg + lane : safe;
+        const int c0 = open ? B.col_idx[idx] : 0;
+        const double v0 = open ? B.val[idx] : 1.0;
+        cv[g] = in ? c0 : lane;
+        vv[g] = in ? v0 : 1.0;
+        if (!in) {
+            lbv[g] = 0.0;
+            ubv[g] = 0.0;
+        }
     }
     int verdict = CLS_DONE, vstatus = status;  // lane g: outcome of instance g
 #pragma unroll

@@ -18,18 +18,39 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent.parent
 
 
+def short(name):
+    """'(anonymous namespace)::halda_solve_k1_kernel(halda_batch, ...)' -> 'halda_solve_k1_kernel'."""
+    return name.split("(")[-2].split("::")[-1] if "::" in name else name.split("(")[0]
+
+
 def per_kernel(csv_path, counter):
     vals = defaultdict(list)
     for r in csv.DictReader(open(csv_path)):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return vals
+
+
+def by_grid(trace_csv, out_csv):
+    """Per (kernel, grid size) launch statistics: separates the C3 launches from the bench's small
+    time-to-optimal launches (the --stats summary averages over both)."""
+    d = defaultdict(list)
+    for r in csv.DictReader(open(trace_csv)):
+        if "halda" in r["Kernel_Name"]:
+            d[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
+                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    with open(out_csv, "w") as f:
+        f.write('"Name","Grid_Size_X","Calls","AverageNs","MinNs","MaxNs"\n')
+        for (k, g), v in sorted(d.items()):
+            f.write(f'"{k}",{g},{len(v)},{statistics.mean(v):.1f},{min(v)},{max(v)}\n')
 
 
 def main(R):
     src = REPO / "gpurun_out" / f"prof_{R}"
     dst = REPO / "profiles"
     shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{R}_kernel_stats.csv")
+    shutil.copy(src / "trace_bench.json", dst / f"{R}_bench_under_rocprof.json")
+    by_grid(src / "trace" / "run_kernel_trace.csv", dst / f"{R}_kernel_by_grid.csv")
     fetch = per_kernel(src / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
     write = per_kernel(src / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
     cal = per_kernel(src / "calib" / "run_counter_collection.csv", "FETCH_SIZE")
@@ -49,7 +70,7 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-    solve = out["kernels"].get("halda_solve_kernel")
+    solve = out["kernels"].get("halda_solve_k1_kernel")
     out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
     out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
                    "coalesced read (tools/hbm_calib.hip), the solve kernel's dominant access width; "
