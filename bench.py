@@ -56,28 +56,37 @@ def build_workload(rank: int, fleets: int, M: int):
 
 
 def algorithmic_bytes(lowered, batch, refs):
-    """Bytes each kernel of one launch sequence must move, as (k1_solve, screen).
+    """Bytes each launch must move: {kernel name: bytes per launch}.
 
-    k = 1 kernel (the dominant one): for every instance that survives the screen, its fleet's CSR
-    (row_ptr + col_idx/val; counted once per fleet), its header, c / col_lb / col_ub (8 B each) and
-    integrality (1 B) per column, row_lb / row_ub per row, x out and the result scalars;
-    screen kernel: for every instance its header (n_cols, n_rows, 3 offsets), the equality row
-    (two row_ptr entries, M col_idx/val, its row bounds), lb/ub of the M w-columns and c[C], the
-    verdict byte, plus the result scalars of the instances it settles."""
+    A solved (surviving) instance: its fleet's CSR once (row_ptr + col_idx/val, which contains the
+    equality row), its header (n_cols, n_rows, 3 offsets), c / col_lb / col_ub (8 B each) and
+    integrality (1 B) per column (which contain the w bounds and c[C]), row_lb / row_ub per row,
+    x out and the result scalars. A screened instance: its header, the equality row (two row_ptr
+    entries, M col_idx/val, its row bounds), lb/ub of its M w-columns, c[C] and the verdict byte,
+    plus the result scalars when the screen settles it (M > W = L/k).
+      halda_screen_k1_kernel (default, one wave per instance): settled instances' screen bytes +
+        survivors' solve bytes + the verdict byte of every instance;
+      halda_screen_kernel + halda_solve_k1_kernel (HALDA_TWO_PASS=1): every instance's screen
+        bytes, then the survivors' solve bytes."""
     hdr, res = 4 + 4 + 8 + 8 + 8, 4 + 8 + 8 + 8 + 8
-    solve, screen = 0, 0
+    solve, screen, fused = 0, 0, 0
     fleets_solved = set()
     for ref in refs:
         fl = lowered[ref.fleet]
-        screen += hdr + 8 + 12 * fl.M + 16 + 16 * fl.M + 8 + 1
+        scr = hdr + 8 + 12 * fl.M + 16 + 16 * fl.M + 8 + 1
+        screen += scr
         if ref.W - fl.M >= 0:
             if ref.fleet not in fleets_solved:
                 fleets_solved.add(ref.fleet)
                 solve += 4 * (fl.n_rows + 1) + 12 * fl.nnz
-            solve += hdr + 25 * fl.n_cols + 16 * fl.n_rows + 8 * fl.n_cols + res
+                fused += 4 * (fl.n_rows + 1) + 12 * fl.nnz
+            one = hdr + 25 * fl.n_cols + 16 * fl.n_rows + 8 * fl.n_cols + res
+            solve += one
+            fused += one + 1
         else:
             screen += res
-    return solve, screen
+            fused += scr + res
+    return {"halda_screen_k1_kernel": fused, "halda_screen_kernel": screen, "halda_solve_k1_kernel": solve}
 
 
 def to_device(batch, torch, dev):
@@ -254,11 +263,8 @@ def main():
 
     total_inst = batch.n_inst * world * args.steps
     value = total_inst / elapsed
-    alg_solve, alg_screen = algorithmic_bytes(lowered, batch, refs)
-    # every surviving C3 instance is k = 1 (M = 64 <= 64): the k = 1 kernel moves the solve bytes;
-    # the general kernel only scans the verdict bytes (no C3 instance is routed to it)
-    alg = {"halda_screen_kernel": alg_screen, "halda_solve_k1_kernel": alg_solve,
-           "halda_solve_kernel": batch.n_inst}[dom]
+    alg_bytes = algorithmic_bytes(lowered, batch, refs)
+    alg = alg_bytes.get(dom, batch.n_inst)  # the general kernel alone only scans the verdict bytes
     solve_ms = phase_ms[dom]
     achieved = alg / (solve_ms * 1e-3) / 1e9
     traffic = pmc_traffic(dom)
@@ -300,7 +306,7 @@ def main():
                 "algorithmic_bytes_per_launch": alg,
                 "sequence_ms": seq_ms,
                 "launch_ms": phase_ms,
-                "algorithmic_bytes": {"halda_screen_kernel": alg_screen, "halda_solve_k1_kernel": alg_solve},
+                "algorithmic_bytes": alg_bytes,
             },
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,

@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -1685,6 +1686,115 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
     }
 }
 
+// Screen of ONE instance by one wave (lane = device): the same verdicts as
+// screen_group. Returns the class; settles (and writes) everything but CLS_K1 /
+// CLS_GEN. Uniform header values are returned for the solve.
+struct Head {
+    int N, m, M;
+    int64_t co, ro, cs;
+    double Wd, kc;
+};
+
+__device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t inst, int lane,
+                                 int mmax, int r1max, int tab, int tab_kc, Head &h) {
+    h.N = B.n_cols[inst];
+    h.m = B.n_rows[inst];
+    h.co = B.col_off[inst];
+    h.ro = B.row_off[inst];
+    h.cs = B.csr_off[inst];
+    int status = 0;
+    if (h.N < 1 || (h.N - 1) % 7 != 0 || h.m < 1) status = HALDA_STATUS_UNSUPPORTED;
+    h.M = status ? 0 : (h.N - 1) / 7;
+    if (!status && h.M > mmax) status = HALDA_STATUS_TOO_LARGE;
+    const int M = h.M, ma = max(h.m, 1);
+    // round trip 2 (branch-free): equality-row extent and bounds, c[C], this lane's w bounds
+    const int32_t *rp = B.row_ptr + h.cs;
+    const int eqs = rp[ma - 1], eqe = rp[ma];
+    const double Wd = B.row_ub[h.ro + ma - 1], Wl = B.row_lb[h.ro + ma - 1];
+    const double cC = B.c[h.co + 7 * int64_t(M)];
+    const int li = lane < M ? lane : 0;
+    double lb = B.col_lb[h.co + li], ub = B.col_ub[h.co + li];
+    h.Wd = Wd;
+    h.kc = cC;
+    if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
+        status = HALDA_STATUS_UNSUPPORTED;
+    int verdict = CLS_DONE;
+    if (!status) {
+        // round trip 3: the equality row (lane = device)
+        const int c0 = B.col_idx[eqs + li];
+        const double v0 = B.val[eqs + li];
+        int bad = 0, infeas = 0, sumlo = 0;
+        auto one = [&](int i, int col, double v, double l, double u) {
+            bad |= col != i || v != 1.0;
+            const int wlo = int(ceil(l)), whi = int(floor(fmin(u, Wd)));
+            infeas |= wlo > whi || l < 0.0;
+            sumlo += wlo;
+        };
+        if (lane < M) one(lane, c0, v0, lb, ub);
+        for (int i = lane + 64; i < M; i += 64) one(i, B.col_idx[eqs + i], B.val[eqs + i], B.col_lb[h.co + i], B.col_ub[h.co + i]);
+        bad = wave_or(bad | (infeas << 1));
+        sumlo = wave_sum(sumlo);
+        const int W = int(Wd);
+        if (bad & 1) status = HALDA_STATUS_UNSUPPORTED;
+        else if ((bad & 2) || sumlo > W || (M == 0 && W > 0)) status = HALDA_STATUS_INFEASIBLE;
+        else if (M == 0) status = 1000;  // no devices and W = 0: optimal, x = [C = 0]
+        else {
+            const int R1 = W - sumlo + 1;
+            const bool kc = cC > 0.0;
+            if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
+            else verdict = (kc || M > kK1MaxM) ? CLS_GEN : CLS_K1;
+        }
+    }
+    if (lane == 0) {
+        cls[inst] = uint8_t(verdict);
+        if (verdict == CLS_DONE) {
+            if (status == 1000) {
+                Rz.x[h.co] = 0.0;
+                Rz.status[inst] = HALDA_STATUS_OPTIMAL;
+                Rz.obj_lin[inst] = Rz.dual_bound[inst] = Rz.gap[inst] = 0.0;
+                Rz.nodes[inst] = 0;
+            } else {
+                write_done(Rz, int(inst), status, 0);
+            }
+        }
+    }
+    return verdict;
+}
+
+// Screen + k = 1 fast path, one wave per instance: a settled instance's wave
+// exits after three round trips, so the hardware dispatcher refills its slot at
+// once and the (fewer, longer) solves stay evenly spread over the chip whatever
+// the order of the survivors in the batch. k > 1 and wide instances, and the
+// fast path's hand-backs, go to halda_solve_kernel (launched next) through cls.
+__global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_kernel(halda_batch B, halda_result Rz,
+                                                                                       uint8_t *cls, int mmax,
+                                                                                       int r1max, int tab, int tab_kc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int64_t inst = blockIdx.x;
+    Head h;
+    if (screen_one(B, Rz, cls, inst, lane, mmax, r1max, tab, tab_kc, h) != CLS_K1) return;
+    const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
+    WaveCtx w = {};
+    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
+    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
+    w.cost = reinterpret_cast<double *>(smem + sl.cost);
+    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
+    Inst I;
+    I.inst = int(inst);
+    I.m = h.m;
+    I.M = h.M;
+    I.iC = 7 * h.M;
+    I.invM = 1.0f / float(h.M);
+    I.co = h.co;
+    I.ro = h.ro;
+    I.rp = B.row_ptr + h.cs;
+    I.Wd = h.Wd;
+    I.W = int(h.Wd);
+    I.kc = h.kc;
+    solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane);
+}
+
 // ------------------------------------------------------------------ host side
 thread_local std::string g_err;
 
@@ -1705,6 +1815,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
+    bool two_pass = false;  // HALDA_TWO_PASS=1: separate screen and persistent k = 1 kernels
     void *scratch = nullptr;  // host-API staging
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
@@ -1763,14 +1874,22 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     }
     uint8_t *cls = static_cast<uint8_t *>(ctx->work);
     HIP_TRY(hipEventRecord(ctx->ev0, stream));
-    const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
-    hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out, cls,
-                       mmax, in.max_R1, int(tab), int(tab_kc));
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->evk, stream));
-    // k = 1 fast path: small LDS slice (device records only), persistent grid = resident capacity
-    {
-        const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
+    const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
+    if (!ctx->two_pass) {
+        // one wave per instance: screen, then the k = 1 solve for the survivors
+        int per_cu = 0;
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_screen_k1_kernel), lds1, &per_cu));
+        hipLaunchKernelGGL(halda_screen_k1_kernel, dim3(unsigned(in.n_inst)), dim3(64), size_t(lds1), stream, in, out,
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evk, stream));
+    } else {
+        // two passes: screen kernel (8 instances per wave), then a persistent k = 1 kernel
+        const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
+        hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->evk, stream));
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_kernel), lds1, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
@@ -1830,6 +1949,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     Ctx *c = new Ctx();
     c->device = device_ordinal;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    const char *tp = std::getenv("HALDA_TWO_PASS");
+    c->two_pass = tp && tp[0] == '1';
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess) {

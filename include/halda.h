@@ -119,8 +119,10 @@ int halda_last_kernel_ms(void *ctx, double *ms);
 /* Device time of the last solve's general kernel (halda_solve_kernel) alone, in ms. */
 int halda_last_solve_kernel_ms(void *ctx, double *ms);
 
-/* Device time of the last solve per launch, in ms: ms3[0] the screen kernel,
- * ms3[1] the k = 1 fast-path kernel, ms3[2] the general kernel. */
+/* Device time of the last solve per launch, in ms: ms3[0] the screen + k = 1
+ * kernel (halda_screen_k1_kernel; with HALDA_TWO_PASS=1 in the environment the
+ * screen kernel alone), ms3[1] 0 (two-pass: the persistent k = 1 kernel),
+ * ms3[2] the general kernel. */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */

@@ -70,7 +70,7 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-    solve = out["kernels"].get("halda_solve_k1_kernel")
+    solve = out["kernels"].get("halda_screen_k1_kernel") or out["kernels"].get("halda_solve_k1_kernel")
     out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
     out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
                    "coalesced read (tools/hbm_calib.hip), the solve kernel's dominant access width; "
