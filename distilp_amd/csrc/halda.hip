@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "halda.h"
 
@@ -1795,6 +1796,333 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_k
     solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane);
 }
 
+// ---------------------------------------------------------------- GPU lowering
+// halda_lower_kernel: one wave per fleet, lane = device, writes the fleet's
+// fixed-k MILPs for every k-candidate into the halda_batch layout with fixed
+// per-fleet strides (solve kernels read them unchanged). Restates the host
+// lowering (distilp_amd/solver/lower.py, itself the reference's
+// solve_fixed_k_milp, halda_p_solver.py:59-338, with dense_common.py:25-230):
+// same row order, same zero-dropping, same FP operation order -> the same CSR
+// and vectors bit for bit.
+struct LowerDims {
+    int mmax, n_k;
+    int64_t cols, rows, nnz;  // strides per instance (cols, rows) and per fleet (nnz)
+};
+
+__host__ __device__ inline LowerDims lower_dims(int mmax, int n_k) {
+    LowerDims d;
+    d.mmax = mmax;
+    d.n_k = n_k;
+    d.cols = 7 * int64_t(mmax) + 1;
+    d.rows = 6 * int64_t(mmax) + 1;   // link M, capacity <= M, VRAM <= 2M, cycle 2M, equality 1
+    d.nnz = 26 * int64_t(mmax);       // 2M + 3M + 4M + 16M + M
+    return d;
+}
+
+// Exclusive prefix sum over the wave (all lanes active); total in *tot.
+__device__ inline int wave_excl_scan(int v, int lane, int *tot) {
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    *tot = __shfl(x, 63);
+    return x - v;
+}
+
+// sum_f_over_s (dense_common.py:49-75) for a key/quantisation known present or absent.
+__device__ inline double f_over_s(bool present, double f, double s) {
+    return present ? (s > 0.0 ? 0.0 + f / s : 0.0) : 0.0;
+}
+
+struct LowerOut {
+    halda_batch b;         // arrays written (device pointers, const-cast by the kernel)
+    int32_t *n_cols, *n_rows, *row_ptr, *col_idx;
+    int64_t *csr_off, *col_off, *row_off;
+    double *val, *c, *col_lb, *col_ub, *row_lb, *row_ub, *offs;  // offs[f]: t_comm sum, xi sum, kappa
+    uint8_t *integrality;
+};
+
+__global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_fleets F, const int32_t *ks, int n_k,
+                                                         LowerDims D, LowerOut O) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x;
+    if (f >= F.n_fleets) return;
+    const int64_t d0 = F.dev_off[f];
+    const int M = int(F.dev_off[f + 1] - d0);
+    const int64_t nnz0 = int64_t(f) * D.nnz;       // this fleet's CSR entries
+    const int64_t rp0 = int64_t(f) * (D.rows + 1);  // this fleet's row_ptr segment
+    const double bp = Mo.b_prime;
+    const int iC = 7 * M;
+    int rows = 0;
+    int64_t nnz = 0;
+    // per-block row emission: lane i emits up to 2 rows of <= 8 entries for device i (chunks of 64)
+    auto emit = [&](int nrow_lane, auto &&row_fn) {
+        for (int i0 = 0; i0 < M; i0 += 64) {
+            const int i = i0 + lane;
+            const bool act = i < M;
+            int cnt[2] = {0, 0};
+            int cols[2][8];
+            double vals[2][8];
+            double rhs[2] = {0.0, 0.0};
+            int nr = 0;
+            if (act) nr = row_fn(i, cols, vals, rhs, cnt);
+            (void)nrow_lane;
+            int rtot = 0, ntot = 0;
+            const int rbase = wave_excl_scan(nr, lane, &rtot);
+            const int nbase = wave_excl_scan(cnt[0] + cnt[1], lane, &ntot);
+            for (int q = 0; q < nr; ++q) {
+                const int r = rows + rbase + q;
+                const int64_t e0 = nnz + nbase + (q ? cnt[0] : 0);
+                O.row_ptr[rp0 + r] = int32_t(nnz0 + e0);
+                for (int k = 0; k < cnt[q]; ++k) {
+                    O.col_idx[nnz0 + e0 + k] = cols[q][k];
+                    O.val[nnz0 + e0 + k] = vals[q][k];
+                }
+                for (int j = 0; j < n_k; ++j) {
+                    const int64_t ro = (int64_t(f) * n_k + j) * D.rows;
+                    O.row_lb[ro + r] = -kInf;
+                    O.row_ub[ro + r] = rhs[q];
+                }
+            }
+            rows += rtot;
+            nnz += ntot;
+        }
+    };
+    // append (col, val) when val != 0 (scipy builds its CSC from the dense rows)
+    auto put = [](int (&cc)[8], double (&vv)[8], int &n, int col, double v) {
+        if (v != 0.0) {
+            cc[n] = col;
+            vv[n] = v;
+            ++n;
+        }
+    };
+    // ---- per-device coefficients (lower._device_arrays order)
+    auto coeff = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
+                     double &bcio, double &xi) {
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        const int cls = F.os_class[g];
+        const double Tc = F.T_cpu[g], tkc = F.t_kvcpy_cpu[g], tkg = F.t_kvcpy_gpu[g];
+        const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu_b1[g]);
+        const bool hb = fl & HALDA_DEV_GPU;
+        const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu_b1[g]) : 0.0;
+        const double tg = hb ? F.T_gpu[g] : 1.0;
+        alpha = (cpu + tkc) + (bp / Tc);
+        const double beta = hb ? ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc) : 0.0;
+        b = cls == 1 ? 0.0 : beta;
+        xi = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
+        const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+        bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.c_cpu[g]);
+        const double sd = fmax(1.0, F.s_disk[g]);
+        p_bp = bp / sd;
+        p_b = Mo.b_layer / sd;
+        p_v = cls == 2 ? p_b : p_bp;
+        cst = xi + F.t_comm[g];
+    };
+    // 1. link rows n_i - w_i <= 0
+    emit(1, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+        put(cc[0], vv[0], cn[0], i, -1.0);
+        put(cc[0], vv[0], cn[0], M + i, 1.0);
+        rh[0] = 0.0;
+        return 1;
+    });
+    // 2-4. RAM / Metal capacity rows by set
+    for (int set = 1; set <= 3; ++set) {
+        emit(1, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+            const int64_t g = d0 + i;
+            if (F.os_class[g] != set) return 0;
+            if (set == 2 && !(F.flags[g] & HALDA_DEV_METAL_AVAIL)) return 0;
+            double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+            coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+            put(cc[0], vv[0], cn[0], i, bp);
+            if (set == 3) put(cc[0], vv[0], cn[0], M + i, -bp);
+            put(cc[0], vv[0], cn[0], (1 + set) * M + i, -bp);
+            if (set == 1) rh[0] = double(F.d_avail_ram[g]) - bcio;
+            else if (set == 2) rh[0] = double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
+            else rh[0] = double(F.d_avail_ram[g] + F.swap[g]) - bcio;
+            return 1;
+        });
+    }
+    // 5. VRAM rows: per device the CUDA row, then the Metal row
+    emit(2, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        int q = 0;
+        if (fl & HALDA_DEV_CUDA_OK) {
+            put(cc[q], vv[q], cn[q], M + i, bp);
+            put(cc[q], vv[q], cn[q], 5 * M + i, -bp);
+            rh[q] = double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
+            ++q;
+        }
+        if (fl & HALDA_DEV_METAL_OK) {
+            const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+            put(cc[q], vv[q], cn[q], M + i, bp);
+            put(cc[q], vv[q], cn[q], 5 * M + i, -bp);
+            rh[q] = double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
+            ++q;
+        }
+        return q;
+    });
+    // 6. cycle rows busy + z - C <= -const ; busy + F - z - C <= -const
+    emit(2, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+        double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+        coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+        const double busy[6] = {alpha, b, p_bp, p_b, p_bp, p_v};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            put(cc[q], vv[q], cn[q], i, q == 0 ? busy[0] : busy[0] + p_bp);
+#pragma unroll
+            for (int blk = 1; blk < 6; ++blk) put(cc[q], vv[q], cn[q], blk * M + i, busy[blk]);
+            put(cc[q], vv[q], cn[q], 6 * M + i, q == 0 ? 1.0 : -1.0);
+            put(cc[q], vv[q], cn[q], iC, -1.0);
+            rh[q] = -cst;
+        }
+        return 2;
+    });
+    // 7. equality row sum_i w_i = W (row bounds per k below)
+    {
+        const int r = rows;
+        O.row_ptr[rp0 + r] = int32_t(nnz0 + nnz);
+        for (int i = lane; i < M; i += 64) {
+            O.col_idx[nnz0 + nnz + i] = i;
+            O.val[nnz0 + nnz + i] = 1.0;
+        }
+        nnz += M;
+        rows += 1;
+        if (lane == 0) O.row_ptr[rp0 + rows] = int32_t(nnz0 + nnz);
+    }
+    // ---- per-instance vectors (lane = device) and headers
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = i0 + lane;
+        if (i >= M) continue;
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        const int cls = F.os_class[g];
+        double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+        coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+        const double busy[6] = {alpha, b, p_bp, p_b, p_bp, p_v};
+        const double gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1.0 : 0.0;
+        const double scale[6] = {1.0, gpu, cls == 1 ? 1.0 : 0.0, cls == 2 ? 1.0 : 0.0, cls == 3 ? 1.0 : 0.0, gpu};
+        for (int j = 0; j < n_k; ++j) {
+            const double W = double(Mo.L / ks[j]);
+            const int64_t co = (int64_t(f) * n_k + j) * D.cols;
+#pragma unroll
+            for (int blk = 0; blk < 6; ++blk) {
+                O.c[co + blk * M + i] = busy[blk];
+                O.col_lb[co + blk * M + i] = blk == 0 ? 1.0 : 0.0;
+                O.col_ub[co + blk * M + i] = scale[blk] * W;
+                O.integrality[co + blk * M + i] = 1;
+            }
+            O.c[co + 6 * M + i] = 0.0;
+            O.col_lb[co + 6 * M + i] = 0.0;
+            O.col_ub[co + 6 * M + i] = kInf;
+            O.integrality[co + 6 * M + i] = 0;
+        }
+    }
+    for (int j = lane; j < n_k; j += 64) {
+        const int64_t inst = int64_t(f) * n_k + j;
+        const int64_t co = inst * D.cols, ro = inst * D.rows;
+        const double W = double(Mo.L / ks[j]);
+        O.c[co + iC] = double(ks[j] - 1);
+        O.col_lb[co + iC] = 0.0;
+        O.col_ub[co + iC] = kInf;
+        O.integrality[co + iC] = 0;
+        O.row_lb[ro + rows - 1] = W;
+        O.row_ub[ro + rows - 1] = W;
+        O.n_cols[inst] = 7 * M + 1;
+        O.n_rows[inst] = rows;
+        O.csr_off[inst] = rp0;
+        O.col_off[inst] = co;
+        O.row_off[inst] = ro;
+    }
+    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230)
+    if (lane == 0) {
+        double tsum = 0.0, xsum = 0.0;
+        int hi = -1;
+        for (int i = 0; i < M; ++i) {
+            const int64_t g = d0 + i;
+            tsum += F.t_comm[g];
+            xsum += (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
+            if (hi < 0 && (F.flags[g] & HALDA_DEV_HEAD)) hi = i;
+        }
+        const int64_t h = d0 + (hi < 0 ? 0 : hi);
+        double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
+        total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
+        total += Mo.b_in / (Mo.V * F.s_disk[h]);
+        total += Mo.b_out / F.s_disk[h];
+        double tail = 0.0;
+        for (int set = 1; set <= 3; set += 2)
+            for (int i = 0; i < M; ++i) {
+                const int64_t g = d0 + i;
+                if (F.os_class[g] == set) tail += double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+            }
+        O.offs[3 * f + 0] = tsum;
+        O.offs[3 * f + 1] = xsum;
+        O.offs[3 * f + 2] = total + tail;
+    }
+}
+
+// halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
+// sum xi + kappa (halda_p_solver.py:356-357), best k by ascending k with strict
+// "<" (halda_p_solver.py:407), w / n of the winner (int(round(x)), :350-351).
+__global__ __launch_bounds__(64) void halda_pick_kernel(halda_batch B, halda_result R, halda_fleets F, int n_k,
+                                                        const double *offs, halda_fleet_result out, int64_t xstride) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x;
+    if (f >= F.n_fleets) return;
+    int best_j = -1;
+    double best = kInf;
+    for (int j = 0; j < n_k; ++j) {
+        const int64_t inst = int64_t(f) * n_k + j;
+        const int st = R.status[inst];
+        double obj = kInf;
+        if (st == HALDA_STATUS_OPTIMAL) {
+            const int64_t co = B.col_off[inst];
+            const int N = B.n_cols[inst];
+            double part = 0.0;
+            for (int c = lane; c < N; c += 64) part += B.c[co + c] * R.x[co + c];
+            obj = wave_sum_f64(part);
+            obj = obj + offs[3 * f + 0];
+            obj = obj + offs[3 * f + 1];
+            obj = obj + offs[3 * f + 2];
+            if (obj < best) {
+                best = obj;
+                best_j = j;
+            }
+        }
+        if (lane == 0) {
+            if (out.obj_by_k) out.obj_by_k[inst] = obj;
+            if (out.status) out.status[inst] = st;
+        }
+        if (out.x || out.c) {
+            const int64_t co = B.col_off[inst];
+            const int N = B.n_cols[inst];
+            for (int cc = lane; cc < N; cc += 64) {
+                if (out.x) out.x[inst * xstride + cc] = st == HALDA_STATUS_OPTIMAL ? R.x[co + cc] : 0.0;
+                if (out.c) out.c[inst * xstride + cc] = B.c[co + cc];
+            }
+        }
+    }
+    const int64_t d0 = F.dev_off[f];
+    const int M = int(F.dev_off[f + 1] - d0);
+    if (lane == 0) {
+        out.best_k[f] = best_j >= 0 ? int(B.c[B.col_off[int64_t(f) * n_k + best_j] + 7 * M]) + 1 : 0;
+        out.obj_value[f] = best;
+    }
+    for (int i = lane; i < M; i += 64) {
+        int w = 0, n = 0;
+        if (best_j >= 0) {
+            const int64_t co = B.col_off[int64_t(f) * n_k + best_j];
+            w = int(rint(R.x[co + i]));
+            n = int(rint(R.x[co + M + i]));
+        }
+        out.w[d0 + i] = w;
+        out.n[d0 + i] = n;
+    }
+}
+
 // ------------------------------------------------------------------ host side
 thread_local std::string g_err;
 
@@ -1816,10 +2144,17 @@ struct Ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
     bool two_pass = false;  // HALDA_TWO_PASS=1: separate screen and persistent k = 1 kernels
-    void *scratch = nullptr;  // host-API staging
+    void *scratch = nullptr;  // host-API staging (device)
+    void *pinned = nullptr;   // host-API staging (pinned host), one PCIe copy each way
+    size_t pinned_bytes = 0;
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
     size_t work_bytes = 0;
+    void *fleet_scratch = nullptr;  // lowered batch + results of halda_solve_fleets
+    size_t fleet_scratch_bytes = 0;
+    halda_batch last_lowered = {};
+    halda_result last_solved = {};
+    bool have_lowered = false;
     // resident workgroups per CU by (kernel, dynamic LDS), raising the LDS limit once per size
     struct Occ {
         const void *fn;
@@ -1966,7 +2301,9 @@ void halda_free(void *ctx) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->work) (void)hipFree(c->work);
+    if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evs) (void)hipEventDestroy(c->evs);
@@ -2028,6 +2365,224 @@ int halda_debug_stamps(unsigned long long *out, int n_inst) {
     return n;
 }
 #endif
+
+int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                       int32_t n_k, halda_fleet_result *out, void *stream) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL ctx/model/fleets/ks/out");
+    const halda_fleets &F = *fleets;
+    if (F.n_fleets <= 0) return HALDA_OK;
+    if (n_k <= 0 || n_k > 1024) return fail(HALDA_E_ARG, "n_k must be in 1..1024");
+    if (F.min_devices < 1 || F.max_devices < F.min_devices || F.max_devices > 4096)
+        return fail(HALDA_E_ARG, "halda_fleets: need 1 <= min_devices <= max_devices <= 4096");
+    if (!F.dev_off || !F.os_class || !F.flags || !F.scpu_b1 || !F.sgpu_b1 || !F.T_cpu || !F.T_gpu ||
+        !F.t_kvcpy_cpu || !F.t_kvcpy_gpu || !F.t_ram2vram || !F.t_vram2ram || !F.t_comm || !F.s_disk ||
+        !F.d_avail_ram || !F.c_cpu || !F.c_gpu || !F.d_avail_cuda || !F.d_avail_metal || !F.swap)
+        return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
+    if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
+    if (model->L < 1) return fail(HALDA_E_ARG, "model.L < 1");
+    // ks (host memory): ascending, unique, positive; staged into the scratch below
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    const int32_t *kh = ks;
+    for (int j = 0; j < n_k; ++j)
+        if (kh[j] < 1 || (j && kh[j] <= kh[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    const LowerDims D = lower_dims(F.max_devices, n_k);
+    const int64_t n_inst = int64_t(F.n_fleets) * n_k;
+    if (n_inst > (int64_t(1) << 30) || int64_t(F.n_fleets) * D.nnz > (int64_t(1) << 31) - 1)
+        return fail(HALDA_E_ARG, "batch too large for one call");
+    // scratch layout
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_ncols = take(4 * n_inst), o_nrows = take(4 * n_inst), o_csr = take(8 * n_inst),
+                 o_col = take(8 * n_inst), o_row = take(8 * n_inst),
+                 o_rp = take(4 * size_t(F.n_fleets) * size_t(D.rows + 1)), o_ci = take(4 * size_t(F.n_fleets) * D.nnz),
+                 o_val = take(8 * size_t(F.n_fleets) * D.nnz), o_c = take(8 * n_inst * D.cols),
+                 o_clb = take(8 * n_inst * D.cols), o_cub = take(8 * n_inst * D.cols),
+                 o_rlb = take(8 * n_inst * D.rows), o_rub = take(8 * n_inst * D.rows), o_int = take(n_inst * D.cols),
+                 o_offs = take(24 * size_t(F.n_fleets)), o_st = take(4 * n_inst), o_x = take(8 * n_inst * D.cols),
+                 o_obj = take(8 * n_inst), o_db = take(8 * n_inst), o_gap = take(8 * n_inst), o_nodes = take(8 * n_inst),
+                 o_ks = take(4 * size_t(n_k));
+    if (off > c->fleet_scratch_bytes) {
+        if (c->fleet_scratch) HIP_TRY(hipFree(c->fleet_scratch));
+        c->fleet_scratch = nullptr;
+        c->fleet_scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&c->fleet_scratch, off));
+        c->fleet_scratch_bytes = off;
+    }
+    char *base = static_cast<char *>(c->fleet_scratch);
+    // the k list travels with the stream (pageable source: the copy is staged before the call returns)
+    int32_t *ks_dev = reinterpret_cast<int32_t *>(base + o_ks);
+    HIP_TRY(hipMemcpyAsync(ks_dev, ks, sizeof(int32_t) * size_t(n_k), hipMemcpyHostToDevice, s));
+    LowerOut O;
+    O.n_cols = reinterpret_cast<int32_t *>(base + o_ncols);
+    O.n_rows = reinterpret_cast<int32_t *>(base + o_nrows);
+    O.csr_off = reinterpret_cast<int64_t *>(base + o_csr);
+    O.col_off = reinterpret_cast<int64_t *>(base + o_col);
+    O.row_off = reinterpret_cast<int64_t *>(base + o_row);
+    O.row_ptr = reinterpret_cast<int32_t *>(base + o_rp);
+    O.col_idx = reinterpret_cast<int32_t *>(base + o_ci);
+    O.val = reinterpret_cast<double *>(base + o_val);
+    O.c = reinterpret_cast<double *>(base + o_c);
+    O.col_lb = reinterpret_cast<double *>(base + o_clb);
+    O.col_ub = reinterpret_cast<double *>(base + o_cub);
+    O.row_lb = reinterpret_cast<double *>(base + o_rlb);
+    O.row_ub = reinterpret_cast<double *>(base + o_rub);
+    O.integrality = reinterpret_cast<uint8_t *>(base + o_int);
+    O.offs = reinterpret_cast<double *>(base + o_offs);
+    hipLaunchKernelGGL(halda_lower_kernel, dim3(unsigned(F.n_fleets)), dim3(64), 0, s, *model, F, ks_dev, int(n_k), D,
+                       O);
+    HIP_TRY(hipGetLastError());
+    // the lowered batch and its shape summary (R = W - M with lb(w) = 1 on every device)
+    halda_batch b = {};
+    b.n_inst = int32_t(n_inst);
+    b.max_cols = int32_t(D.cols);
+    int r1_k1 = 0, r1_kc = 0;
+    for (int j = 0; j < n_k; ++j) {
+        const int r1 = model->L / kh[j] - F.min_devices + 1;
+        if (kh[j] == 1) r1_k1 = std::max(r1_k1, r1);
+        else r1_kc = std::max(r1_kc, r1);
+    }
+    b.max_R1 = std::max(1, std::max(r1_k1, r1_kc));
+    if (b.max_R1 > 128) return fail(HALDA_E_ARG, "L / k_min - min_devices + 1 > 128 (layers beyond one per device)");
+    b.max_tab = r1_k1 > 0 ? F.max_devices * r1_k1 : 0;
+    b.max_tab_kc = r1_kc > 0 ? F.max_devices * r1_kc : 0;
+    b.n_cols = O.n_cols;
+    b.n_rows = O.n_rows;
+    b.csr_off = O.csr_off;
+    b.col_off = O.col_off;
+    b.row_off = O.row_off;
+    b.row_ptr = O.row_ptr;
+    b.col_idx = O.col_idx;
+    b.val = O.val;
+    b.c = O.c;
+    b.col_lb = O.col_lb;
+    b.col_ub = O.col_ub;
+    b.row_lb = O.row_lb;
+    b.row_ub = O.row_ub;
+    b.integrality = O.integrality;
+    b.mip_rel_gap = 0.0;
+    b.mip_abs_gap = 0.0;
+    b.time_limit = 0.0;
+    halda_result r;
+    r.status = reinterpret_cast<int32_t *>(base + o_st);
+    r.x = reinterpret_cast<double *>(base + o_x);
+    r.obj_lin = reinterpret_cast<double *>(base + o_obj);
+    r.dual_bound = reinterpret_cast<double *>(base + o_db);
+    r.gap = reinterpret_cast<double *>(base + o_gap);
+    r.nodes = reinterpret_cast<int64_t *>(base + o_nodes);
+    const int rc = launch(c, b, r, s);
+    if (rc != HALDA_OK) return rc;
+    hipLaunchKernelGGL(halda_pick_kernel, dim3(unsigned(F.n_fleets)), dim3(64), 0, s, b, r, F, int(n_k),
+                       static_cast<const double *>(O.offs), *out, D.cols);
+    HIP_TRY(hipGetLastError());
+    c->last_lowered = b;
+    c->last_solved = r;
+    c->have_lowered = true;
+    return HALDA_OK;
+}
+
+// Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.
+int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fh, const int32_t *ks,
+                            int32_t n_k, halda_fleet_result *out_h) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !model || !fh || !ks || !out_h) return fail(HALDA_E_ARG, "NULL ctx/model/fleets/ks/out");
+    if (fh->n_fleets <= 0) return HALDA_OK;
+    if (!fh->dev_off) return fail(HALDA_E_ARG, "halda_fleets.dev_off is NULL");
+    const int64_t nf = fh->n_fleets, nd = fh->dev_off[nf];
+    if (nd < nf || n_k <= 0) return fail(HALDA_E_ARG, "bad device count / n_k");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_doff = take(8 * (nf + 1)), o_cls = take(nd), o_fl = take(nd), o_f64 = take(8 * nd * 10),
+                 o_i64 = take(8 * nd * 6), o_bk = take(4 * nf), o_obj = take(8 * nf), o_w = take(4 * nd),
+                 o_n = take(4 * nd), o_obk = take(8 * nf * n_k), o_st = take(4 * nf * n_k);
+    const size_t xs = size_t(nf) * n_k * (7 * size_t(std::max(fh->max_devices, 1)) + 1);
+    const size_t o_x = out_h->x ? take(8 * xs) : 0, o_c = out_h->c ? take(8 * xs) : 0;
+    if (off > c->scratch_bytes) {
+        if (c->scratch) HIP_TRY(hipFree(c->scratch));
+        c->scratch = nullptr;
+        c->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&c->scratch, off));
+        c->scratch_bytes = off;
+    }
+    char *base = static_cast<char *>(c->scratch);
+    // inputs are packed into pinned host memory and cross PCIe in ONE copy (results likewise)
+    if (off > c->pinned_bytes) {
+        if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
+        c->pinned = nullptr;
+        c->pinned_bytes = 0;
+        HIP_TRY(hipHostMalloc(&c->pinned, off, hipHostMallocDefault));
+        c->pinned_bytes = off;
+    }
+    char *pin = static_cast<char *>(c->pinned);
+    auto up = [&](size_t o, const void *src, size_t bytes) {
+        std::memcpy(pin + o, src, bytes);
+        return hipSuccess;
+    };
+    halda_fleets d = *fh;
+    HIP_TRY(up(o_doff, fh->dev_off, 8 * (nf + 1)));
+    HIP_TRY(up(o_cls, fh->os_class, nd));
+    HIP_TRY(up(o_fl, fh->flags, nd));
+    const double *f64[10] = {fh->scpu_b1, fh->sgpu_b1, fh->T_cpu, fh->T_gpu, fh->t_kvcpy_cpu,
+                             fh->t_kvcpy_gpu, fh->t_ram2vram, fh->t_vram2ram, fh->t_comm, fh->s_disk};
+    const int64_t *i64[6] = {fh->d_avail_ram, fh->c_cpu, fh->c_gpu, fh->d_avail_cuda, fh->d_avail_metal, fh->swap};
+    for (int a = 0; a < 10; ++a) {
+        if (!f64[a] || !fh->os_class || !fh->flags) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
+        HIP_TRY(up(o_f64 + 8 * nd * a, f64[a], 8 * nd));
+    }
+    for (int a = 0; a < 6; ++a) {
+        if (!i64[a]) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
+        HIP_TRY(up(o_i64 + 8 * nd * a, i64[a], 8 * nd));
+    }
+    HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));
+    auto F64 = [&](int a) { return reinterpret_cast<const double *>(base + o_f64 + 8 * nd * a); };
+    auto I64 = [&](int a) { return reinterpret_cast<const int64_t *>(base + o_i64 + 8 * nd * a); };
+    d.dev_off = reinterpret_cast<const int64_t *>(base + o_doff);
+    d.os_class = reinterpret_cast<const uint8_t *>(base + o_cls);
+    d.flags = reinterpret_cast<const uint8_t *>(base + o_fl);
+    d.scpu_b1 = F64(0); d.sgpu_b1 = F64(1); d.T_cpu = F64(2); d.T_gpu = F64(3); d.t_kvcpy_cpu = F64(4);
+    d.t_kvcpy_gpu = F64(5); d.t_ram2vram = F64(6); d.t_vram2ram = F64(7); d.t_comm = F64(8); d.s_disk = F64(9);
+    d.d_avail_ram = I64(0); d.c_cpu = I64(1); d.c_gpu = I64(2); d.d_avail_cuda = I64(3); d.d_avail_metal = I64(4);
+    d.swap = I64(5);
+    halda_fleet_result r;
+    r.best_k = reinterpret_cast<int32_t *>(base + o_bk);
+    r.obj_value = reinterpret_cast<double *>(base + o_obj);
+    r.w = reinterpret_cast<int32_t *>(base + o_w);
+    r.n = reinterpret_cast<int32_t *>(base + o_n);
+    r.obj_by_k = reinterpret_cast<double *>(base + o_obk);
+    r.status = reinterpret_cast<int32_t *>(base + o_st);
+    r.x = out_h->x ? reinterpret_cast<double *>(base + o_x) : nullptr;
+    r.c = out_h->c ? reinterpret_cast<double *>(base + o_c) : nullptr;
+    const int rc = halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
+    if (rc != HALDA_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(pin + o_bk, base + o_bk, off - o_bk, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    auto down = [&](void *dst, size_t o, size_t bytes) {
+        if (dst) std::memcpy(dst, pin + o, bytes);
+        return hipSuccess;
+    };
+    HIP_TRY(down(out_h->best_k, o_bk, 4 * nf));
+    HIP_TRY(down(out_h->obj_value, o_obj, 8 * nf));
+    HIP_TRY(down(out_h->w, o_w, 4 * nd));
+    HIP_TRY(down(out_h->n, o_n, 4 * nd));
+    HIP_TRY(down(out_h->obj_by_k, o_obk, 8 * nf * n_k));
+    HIP_TRY(down(out_h->status, o_st, 4 * nf * n_k));
+    HIP_TRY(down(out_h->x, o_x, 8 * xs));
+    HIP_TRY(down(out_h->c, o_c, 8 * xs));
+    HIP_TRY(hipStreamSynchronize(s));
+    return HALDA_OK;
+}
+
+int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !lowered || !solved) return fail(HALDA_E_ARG, "NULL ctx/lowered/solved");
+    if (!c->have_lowered) return fail(HALDA_E_ARG, "no halda_solve_fleets call on this context");
+    *lowered = c->last_lowered;
+    *solved = c->last_solved;
+    return HALDA_OK;
+}
 
 int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
     Ctx *c = static_cast<Ctx *>(ctx);

@@ -1,0 +1,302 @@
+"""Whole k-sweeps on the GPU from a flat device-field table (libhalda `halda_solve_fleets`).
+
+`halda_solve` (halda.py) keeps the reference's host lowering so its objective is
+formed by NumPy exactly as the reference forms it. This module is the
+throughput / streaming path above the same kernels: fleets are packed into a
+`FleetTable` (one entry per device, the fields the reference's formulas read,
+dense_common.py:25-230), and libhalda lowers every (fleet, k) on the GPU
+(bit-identical CSR to `lower.lower_fleet`), solves it and keeps the best k by the
+reference's rule (ascending k, strict "<", halda_p_solver.py:407). Only the
+table goes over PCIe (~1.9 KB per 64-device fleet instead of ~160 KB of lowered
+MILPs), and re-profiled fleets (config C5) never touch per-device Python
+objects: `FleetTable.perturbed` rescales the table directly.
+
+obj_value here is c.x + sum t_comm + sum xi + kappa formed on the GPU with c.x
+summed in a fixed tree order: within 1e-12 relative of NumPy's dot (the host
+path's). The table builder raises the reference's exceptions (ValueError for a
+FLOPs table without batch key b_1, ZeroDivisionError for T_cpu == 0 or a zero
+s_disk the objective constant divides by).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, replace
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from ..common import DeviceProfile, ModelProfile
+from ._libhalda import HaldaBatchC, HaldaResultC, get_context, last_error
+from .coefficients import HALDAResult, assign_sets, b_prime, gpu_flops_table, gpu_load_throughput
+from .lower import kv_bits_to_factor
+
+DEV_HEAD, DEV_UMA, DEV_CPU_RATE, DEV_GPU, DEV_GPU_RATE, DEV_CUDA_OK, DEV_METAL_OK, DEV_METAL_AVAIL = (
+    1, 2, 4, 8, 16, 32, 64, 128)
+
+F64_FIELDS = ("scpu_b1", "sgpu_b1", "T_cpu", "T_gpu", "t_kvcpy_cpu", "t_kvcpy_gpu", "t_ram2vram", "t_vram2ram",
+              "t_comm", "s_disk")
+I64_FIELDS = ("d_avail_ram", "c_cpu", "c_gpu", "d_avail_cuda", "d_avail_metal", "swap")
+
+
+class HaldaModelC(ctypes.Structure):
+    _fields_ = [("f_q_b1", ctypes.c_double), ("f_out_b1", ctypes.c_double), ("has_f_q", ctypes.c_int32),
+                ("has_f_out", ctypes.c_int32), ("b_prime", ctypes.c_double), ("b_layer", ctypes.c_double),
+                ("b_in", ctypes.c_double), ("b_out", ctypes.c_double), ("V", ctypes.c_double), ("L", ctypes.c_int32)]
+
+
+class HaldaFleetsC(ctypes.Structure):
+    _fields_ = ([("n_fleets", ctypes.c_int32), ("min_devices", ctypes.c_int32), ("max_devices", ctypes.c_int32),
+                 ("dev_off", ctypes.c_void_p), ("os_class", ctypes.c_void_p), ("flags", ctypes.c_void_p)]
+                + [(f, ctypes.c_void_p) for f in F64_FIELDS] + [(f, ctypes.c_void_p) for f in I64_FIELDS])
+
+
+class HaldaFleetResultC(ctypes.Structure):
+    _fields_ = [("best_k", ctypes.c_void_p), ("obj_value", ctypes.c_void_p), ("w", ctypes.c_void_p),
+                ("n", ctypes.c_void_p), ("obj_by_k", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("x", ctypes.c_void_p), ("c", ctypes.c_void_p)]
+
+
+def _bind(lib):
+    if getattr(lib, "_fleets_bound", False):
+        return lib
+    lib.halda_solve_fleets.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaModelC), ctypes.POINTER(HaldaFleetsC),
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(HaldaFleetResultC),
+                                       ctypes.c_void_p]
+    lib.halda_solve_fleets.restype = ctypes.c_int
+    lib.halda_solve_fleets_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaModelC),
+                                            ctypes.POINTER(HaldaFleetsC), ctypes.c_void_p, ctypes.c_int32,
+                                            ctypes.POINTER(HaldaFleetResultC)]
+    lib.halda_solve_fleets_host.restype = ctypes.c_int
+    lib.halda_last_lowered.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC), ctypes.POINTER(HaldaResultC)]
+    lib.halda_last_lowered.restype = ctypes.c_int
+    lib._fleets_bound = True
+    return lib
+
+
+def model_struct(model: ModelProfile, kv_factor: float) -> HaldaModelC:
+    m = HaldaModelC()
+    m.has_f_q = int("b_1" in model.f_q)
+    m.f_q_b1 = float(model.f_q["b_1"]) if m.has_f_q else 0.0
+    m.has_f_out = int("b_1" in model.f_out)
+    m.f_out_b1 = float(model.f_out["b_1"]) if m.has_f_out else 0.0
+    m.b_prime = float(b_prime(model, kv_bits_k=kv_factor))
+    m.b_layer, m.b_in, m.b_out, m.V = float(model.b_layer), float(model.b_in), float(model.b_out), float(model.V)
+    m.L = int(model.L)
+    return m
+
+
+@dataclass
+class FleetTable:
+    """Device fields of many fleets, one entry per device (fleet f = devices dev_off[f] .. dev_off[f+1]-1)."""
+
+    dev_off: np.ndarray  # int64 [n_fleets + 1]
+    os_class: np.ndarray  # uint8: 1 M1, 2 M2, 3 M3
+    flags: np.ndarray  # uint8 DEV_*
+    scpu_b1: np.ndarray
+    sgpu_b1: np.ndarray
+    T_cpu: np.ndarray
+    T_gpu: np.ndarray
+    t_kvcpy_cpu: np.ndarray
+    t_kvcpy_gpu: np.ndarray
+    t_ram2vram: np.ndarray
+    t_vram2ram: np.ndarray
+    t_comm: np.ndarray
+    s_disk: np.ndarray
+    d_avail_ram: np.ndarray  # int64
+    c_cpu: np.ndarray
+    c_gpu: np.ndarray
+    d_avail_cuda: np.ndarray
+    d_avail_metal: np.ndarray
+    swap: np.ndarray
+
+    @property
+    def n_fleets(self) -> int:
+        return int(self.dev_off.shape[0] - 1)
+
+    @property
+    def n_devices(self) -> int:
+        return int(self.dev_off[-1])
+
+    def sizes(self) -> np.ndarray:
+        return np.diff(self.dev_off)
+
+    def sets(self, f: int):
+        """{"M1", "M2", "M3"} index lists of fleet f (dense_common.py:149-167)."""
+        cls = self.os_class[self.dev_off[f]:self.dev_off[f + 1]]
+        return {f"M{s}": [int(i) for i in np.nonzero(cls == s)[0]] for s in (1, 2, 3)}
+
+    def perturbed(self, rng: np.random.Generator, lo: float = 0.9, hi: float = 1.1) -> "FleetTable":
+        """Every numeric field times an independent log-uniform factor in [lo, hi] (config C5: a
+        re-profiled fleet); byte counts stay integers (floor). Flags and device classes are kept."""
+        n = self.n_devices
+
+        def lu():
+            return np.exp(rng.uniform(np.log(lo), np.log(hi), n))
+
+        upd = {f: getattr(self, f) * lu() for f in F64_FIELDS}
+        upd.update({f: np.floor(getattr(self, f) * lu()).astype(np.int64) for f in I64_FIELDS})
+        return replace(self, **upd)
+
+    def check(self) -> None:
+        """The reference's ZeroDivisionErrors (alpha: bp / T_cpu; kappa: head and M1/M3 s_disk)."""
+        if np.any(self.T_cpu == 0.0):
+            raise ZeroDivisionError("float division by zero")
+        head = self.flags & DEV_HEAD
+        for f in range(self.n_fleets):
+            a, b = self.dev_off[f], self.dev_off[f + 1]
+            hs = np.nonzero(head[a:b])[0]
+            h = a + (int(hs[0]) if len(hs) else 0)
+            if self.s_disk[h] == 0.0 or np.any((self.os_class[a:b] != 2) & (self.s_disk[a:b] == 0.0)):
+                raise ZeroDivisionError("float division by zero")
+
+
+def _rate(table, q) -> tuple:
+    """(present, value) of sum_f_over_s's S[q]["b_1"] (dense_common.py:49-75)."""
+    if table is None or q not in table:
+        return False, 0.0
+    row = table[q]
+    if "b_1" not in row:
+        raise ValueError(f"Batch size 1 (key 'b_1') not found in S_by_q[{q}]")
+    return True, float(row["b_1"])
+
+
+def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
+    """Pack fleets (lists of DeviceProfile) into a FleetTable."""
+    Q = model.Q
+    cls, flags, cols = [], [], {f: [] for f in F64_FIELDS + I64_FIELDS}
+    off = [0]
+    for devs in fleets:
+        if not devs:
+            raise IndexError("list index out of range")  # the reference's kappa on an empty fleet
+        for d in devs:
+            cls.append({"mac_no_metal": 1, "mac_metal": 2}.get(d.os_type, 3))
+            fl = (DEV_HEAD if d.is_head else 0) | (DEV_UMA if d.is_unified_mem else 0)
+            ok, v = _rate(d.scpu, Q)
+            fl |= DEV_CPU_RATE if ok else 0
+            table, tg = gpu_flops_table(d), gpu_load_throughput(d)
+            gv, tgv = 0.0, 1.0
+            if table is not None and tg is not None:
+                fl |= DEV_GPU
+                gok, gv = _rate(table, Q)
+                fl |= DEV_GPU_RATE if gok else 0
+                tgv = float(tg)
+            fl |= DEV_CUDA_OK if (d.has_cuda and d.d_avail_cuda is not None) else 0
+            fl |= DEV_METAL_OK if (d.has_metal and d.d_avail_metal is not None) else 0
+            fl |= DEV_METAL_AVAIL if d.d_avail_metal is not None else 0
+            flags.append(fl)
+            c = cols
+            c["scpu_b1"].append(v)
+            c["sgpu_b1"].append(gv)
+            c["T_cpu"].append(d.T_cpu)
+            c["T_gpu"].append(tgv)
+            c["t_kvcpy_cpu"].append(d.t_kvcpy_cpu)
+            c["t_kvcpy_gpu"].append(d.t_kvcpy_gpu)
+            c["t_ram2vram"].append(d.t_ram2vram)
+            c["t_vram2ram"].append(d.t_vram2ram)
+            c["t_comm"].append(d.t_comm)
+            c["s_disk"].append(d.s_disk)
+            c["d_avail_ram"].append(d.d_avail_ram)
+            c["c_cpu"].append(d.c_cpu)
+            c["c_gpu"].append(d.c_gpu)
+            c["d_avail_cuda"].append(d.d_avail_cuda or 0)
+            c["d_avail_metal"].append(d.d_avail_metal or 0)
+            c["swap"].append(min(d.d_bytes_can_swap, d.d_swap_avail) if d.os_type == "android" else 0)
+        off.append(off[-1] + len(devs))
+    t = FleetTable(dev_off=np.asarray(off, np.int64), os_class=np.asarray(cls, np.uint8),
+                   flags=np.asarray(flags, np.uint8),
+                   **{f: np.asarray(cols[f], np.float64) for f in F64_FIELDS},
+                   **{f: np.asarray(cols[f], np.int64) for f in I64_FIELDS})
+    t.check()
+    return t
+
+
+@dataclass
+class FleetSolve:
+    """Per fleet: best k (0 = none feasible), obj_value, w / n (device layout); per (fleet, k): obj, status."""
+
+    best_k: np.ndarray
+    obj_value: np.ndarray
+    w: np.ndarray
+    n: np.ndarray
+    obj_by_k: np.ndarray  # [n_fleets, n_k]
+    status: np.ndarray  # [n_fleets, n_k]
+    ks: List[int]
+    x: Optional[np.ndarray] = None  # [n_fleets, n_k, 7 max_devices + 1] when requested
+    c: Optional[np.ndarray] = None
+
+
+def _fleets_struct(t: FleetTable, ptr) -> HaldaFleetsC:
+    s = HaldaFleetsC()
+    s.n_fleets = t.n_fleets
+    sz = t.sizes()
+    s.min_devices, s.max_devices = int(sz.min()), int(sz.max())
+    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS:
+        setattr(s, f, ptr(f))
+    return s
+
+
+def _k_list(model: ModelProfile, k_candidates: Optional[Iterable[int]]) -> List[int]:
+    if k_candidates:
+        return sorted(set(int(k) for k in k_candidates))
+    L = model.L
+    return sorted({d for d in range(1, L) if L % d == 0}) if L > 1 else []
+
+
+def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
+                device: int = 0, want_x: bool = False) -> FleetSolve:
+    """halda_solve_fleets_host on a host FleetTable (synchronous). want_x: also x and the lowered c
+    of every (fleet, k) (so the host can form obj_value exactly as the reference, with NumPy)."""
+    ks = [int(k) for k in ks]
+    if not ks:
+        raise ValueError("no k-candidates")
+    if ks[0] <= 0:
+        raise ZeroDivisionError("integer division or modulo by zero")
+    ctx = get_context(device)
+    lib = _bind(ctx.lib)
+    arrs = {f: np.ascontiguousarray(getattr(table, f)) for f in ("dev_off", "os_class", "flags") + F64_FIELDS
+            + I64_FIELDS}
+    fs = _fleets_struct(table, lambda f: arrs[f].ctypes.data)
+    nf, nd, nk = table.n_fleets, table.n_devices, len(ks)
+    out = FleetSolve(best_k=np.zeros(nf, np.int32), obj_value=np.zeros(nf), w=np.zeros(nd, np.int32),
+                     n=np.zeros(nd, np.int32), obj_by_k=np.zeros((nf, nk)), status=np.zeros((nf, nk), np.int32),
+                     ks=ks)
+    if want_x:
+        xs = 7 * int(fs.max_devices) + 1
+        out.x, out.c = np.zeros((nf, nk, xs)), np.zeros((nf, nk, xs))
+    r = HaldaFleetResultC(out.best_k.ctypes.data, out.obj_value.ctypes.data, out.w.ctypes.data, out.n.ctypes.data,
+                          out.obj_by_k.ctypes.data, out.status.ctypes.data,
+                          out.x.ctypes.data if want_x else None, out.c.ctypes.data if want_x else None)
+    karr = np.asarray(ks, np.int32)
+    m = model_struct(model, kv_factor)
+    with ctx._lock:
+        rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
+                                         ctypes.byref(r))
+    if rc != 0:
+        raise RuntimeError(f"halda_solve_fleets_host failed ({rc}): {last_error(lib)}")
+    return out
+
+
+def halda_solve_fleets(
+    fleets: Sequence[List[DeviceProfile]],
+    model: ModelProfile,
+    k_candidates: Optional[Iterable[int]] = None,
+    mip_gap: Optional[float] = 1e-4,
+    kv_bits: str = "8bit",
+    device: int = 0,
+) -> List[Optional[HALDAResult]]:
+    """Many `halda_solve` calls in one GPU k-sweep (lowering on the GPU). Returns one HALDAResult per
+    fleet, or None where no k is feasible (where `halda_solve` would raise). Prints nothing."""
+    kv_factor = kv_bits_to_factor(kv_bits)
+    ks = _k_list(model, k_candidates)
+    table = fleet_table(fleets, model)
+    res = solve_table(table, model, ks, kv_factor, device)
+    out: List[Optional[HALDAResult]] = []
+    for f, devs in enumerate(fleets):
+        if res.best_k[f] == 0:
+            out.append(None)
+            continue
+        a, b = table.dev_off[f], table.dev_off[f + 1]
+        out.append(HALDAResult(w=[int(v) for v in res.w[a:b]], n=[int(v) for v in res.n[a:b]], k=int(res.best_k[f]),
+                               obj_value=float(res.obj_value[f]), sets=assign_sets(list(devs))))
+    return out

@@ -13,19 +13,26 @@ src/distilp/solver/halda_p_solver.py:59-436. The observable contract kept:
   * best k by strict "<" in ascending k (smallest k wins ties, :407);
   * debug prints and plot_k_curve(...) as in :389-435.
 
-What changed: all k-candidates of the fleet are lowered once to a shared CSR
-and solved in ONE libhalda batch on the GPU (exactly, gap 0), instead of one
-scipy/HiGHS call per k.
+What changed: the fleet goes to libhalda as a device-field table; every
+k-candidate is lowered on the GPU (bit-identical CSR to lower.lower_fleet, the
+host restatement pinned to the reference's arrays) and solved exactly (gap 0)
+in ONE halda_solve_fleets call, instead of one scipy/HiGHS call per k. The
+objective of each k is then formed here with NumPy from the returned c and x,
+exactly as the reference forms it. `halda_solve_batch` keeps the host lowering
+(one CSR per fleet shared by its k-instances through `halda_solve_batch`).
 """
 
 from __future__ import annotations
 
 from typing import Iterable, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from ..common import DeviceProfile, ModelProfile
 from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL, BatchResult, get_context
 from .batch import assemble
-from .coefficients import HALDAResult, ILPResult, assign_sets, valid_factors_of_L
+from .coefficients import HALDAResult, ILPResult, assign_sets, kappa_constant, valid_factors_of_L
+from .fleets import fleet_table, solve_table
 from .lower import FleetMILP, kv_bits_to_factor, lower_fleet
 
 
@@ -53,6 +60,53 @@ def _results_for(fleets: Sequence[FleetMILP], refs, res: BatchResult) -> List[Li
     return out
 
 
+def _offset_parts(devs, model: ModelProfile, sets) -> Tuple[float, float, float]:
+    """(sum t_comm, sum xi, kappa) in the reference's order (halda_p_solver.py:356-357,
+    dense_common.py:100-119, 211-230): the constant part of obj_value."""
+    kappa = kappa_constant(devs, model, sets)  # IndexError on an empty fleet, like the reference
+    t_comm = 0
+    for d in devs:
+        t_comm += d.t_comm
+    xi_sum = 0
+    for d in devs:
+        xi_sum += (d.t_ram2vram + d.t_vram2ram) * (0.0 if d.is_unified_mem else 1.0)
+    return t_comm, xi_sum, kappa
+
+
+def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: float, offsets,
+                  device: int) -> List[Tuple[int, Optional[ILPResult]]]:
+    """Every k of one fleet lowered, solved and returned by ONE halda_solve_fleets call (the CSR is
+    built on the GPU, bit-identical to lower.lower_fleet); obj_value = c.x + offsets formed here with
+    NumPy on the returned c and x, exactly as the reference forms it (halda_p_solver.py:347-357)."""
+    if any(k == 0 for k in Ks):
+        raise ZeroDivisionError("integer division or modulo by zero")  # W = L // k (halda_p_solver.py:76)
+    pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
+    table = fleet_table([devs], model)
+    res = solve_table(table, model, pos, kv_factor, device, want_x=True) if pos else None
+    M, N = len(devs), 7 * len(devs) + 1
+    t_comm, xi_sum, kappa = offsets
+    out: List[Tuple[int, Optional[ILPResult]]] = []
+    for k in Ks:
+        if k < 0:
+            out.append((k, None))
+            continue
+        j = pos.index(k)
+        st = int(res.status[0, j])
+        if st == STATUS_OPTIMAL:
+            x = np.array(res.x[0, j, :N])
+            c = np.array(res.c[0, j, :N])
+            obj = float(c.dot(x)) + t_comm + xi_sum + kappa
+            out.append((k, ILPResult(k=k, w=[int(round(v)) for v in x[:M]], n=[int(round(v)) for v in x[M:2 * M]],
+                                     obj_value=obj)))
+        elif st == STATUS_INFEASIBLE:
+            out.append((k, None))
+        else:
+            raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
+                               "the lowered MILP does not have the HALDA structure")
+    return out
+
+
+
 def _pick(per_k: List[Tuple[int, Optional[ILPResult]]]) -> Optional[ILPResult]:
     best: Optional[ILPResult] = None
     for _, r in per_k:
@@ -74,11 +128,10 @@ def halda_solve(
     """HALDA layer assignment: best k, w, n over the k-candidates (drop-in for the reference)."""
     Ks = _k_list(model, k_candidates)
     kv_factor = kv_bits_to_factor(kv_bits)
+    devs = list(devs)
     sets = assign_sets(devs)
-    fl = lower_fleet(devs, model, kv_factor=kv_factor, sets=sets)
-    batch, refs = assemble([fl], [Ks], mip_gap)
-    res = get_context(device).solve(batch)
-    per_k = _results_for([fl], refs, res)[0]
+    offsets = _offset_parts(devs, model, sets)  # raises the reference's errors on degenerate fleets
+    per_k = _sweep_on_gpu(devs, model, sets, Ks, kv_factor, offsets, device)
 
     if debug:
         print("Objectives by k")

@@ -125,6 +125,79 @@ int halda_last_solve_kernel_ms(void *ctx, double *ms);
  * ms3[2] the general kernel. */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
+/* ------------------------------------------------------------------------
+ * Whole k-sweeps on the GPU: lowering + solve + argmin over k.
+ *
+ * halda_solve_fleets() runs the reference's `halda_solve` for a batch of
+ * fleets (halda_p_solver.py:369-436): per fleet it lowers every k-candidate
+ * to the fixed-k MILP exactly as solve_fixed_k_milp does
+ * (halda_p_solver.py:59-338 with the coefficients of dense_common.py:25-230,
+ * same operation order, bit-identical CSR to the host lowering), solves them
+ * with the kernels above and keeps the best k by the reference's rule
+ * (ascending k, strict "<" on obj_value). Inputs are a flat table of the
+ * device fields the formulas read (one entry per device, fleets contiguous),
+ * so a stream of re-profiled fleets never goes through per-device Python
+ * objects. obj_value = c.x + sum t_comm + sum xi + kappa is formed on the GPU
+ * (c.x summed in a fixed tree order: within 1e-12 relative of NumPy's dot).
+ * ------------------------------------------------------------------------ */
+
+typedef struct halda_model {
+    double f_q_b1;      /* ModelProfile.f_q["b_1"] (when has_f_q) */
+    double f_out_b1;    /* ModelProfile.f_out["b_1"] (when has_f_out) */
+    int32_t has_f_q, has_f_out;
+    double b_prime;     /* b_prime(model, kv) (dense_common.py:25-46), an integer value */
+    double b_layer, b_in, b_out, V;
+    int32_t L;
+} halda_model;
+
+/* halda_fleets.flags bits, per device */
+#define HALDA_DEV_HEAD 1       /* is_head */
+#define HALDA_DEV_UMA 2        /* is_unified_mem */
+#define HALDA_DEV_CPU_RATE 4   /* Q in scpu: scpu_b1 = scpu[Q]["b_1"] */
+#define HALDA_DEV_GPU 8        /* a GPU FLOPs table and load throughput (beta is active) */
+#define HALDA_DEV_GPU_RATE 16  /* ... and Q in that table: sgpu_b1 = table[Q]["b_1"] */
+#define HALDA_DEV_CUDA_OK 32   /* has_cuda and d_avail_cuda is not None */
+#define HALDA_DEV_METAL_OK 64  /* has_metal and d_avail_metal is not None */
+#define HALDA_DEV_METAL_AVAIL 128 /* d_avail_metal is not None (M2 RAM row present) */
+
+typedef struct halda_fleets {
+    int32_t n_fleets;
+    int32_t min_devices, max_devices; /* over the batch (size the scratch and the shape summary) */
+    const int64_t *dev_off;           /* [n_fleets + 1]: fleet f owns devices dev_off[f] .. dev_off[f+1]-1 */
+    const uint8_t *os_class;          /* 1 mac_no_metal (M1), 2 mac_metal (M2), 3 anything else (M3) */
+    const uint8_t *flags;             /* HALDA_DEV_* */
+    const double *scpu_b1, *sgpu_b1;  /* FLOP/s for batch 1 at quantization Q */
+    const double *T_cpu, *T_gpu;      /* T_gpu: the load throughput matching the GPU table */
+    const double *t_kvcpy_cpu, *t_kvcpy_gpu, *t_ram2vram, *t_vram2ram, *t_comm, *s_disk;
+    const int64_t *d_avail_ram, *c_cpu, *c_gpu, *d_avail_cuda, *d_avail_metal;
+    const int64_t *swap;              /* min(d_bytes_can_swap, d_swap_avail) for android, else 0 */
+} halda_fleets;
+
+typedef struct halda_fleet_result {
+    int32_t *best_k;     /* [n_fleets] best k, 0 when no k is feasible */
+    double *obj_value;   /* [n_fleets] */
+    int32_t *w, *n;      /* [dev_off[n_fleets]] device layout */
+    double *obj_by_k;    /* [n_fleets * n_k] obj_value per k (+inf infeasible); may be NULL */
+    int32_t *status;     /* [n_fleets * n_k] HALDA_STATUS_* per k; may be NULL */
+    double *x;           /* [n_fleets * n_k * (7 max_devices + 1)] x per (fleet, k), column layout; may be NULL */
+    double *c;           /* same layout: the lowered objective c per (fleet, k); may be NULL */
+} halda_fleet_result;
+
+/* Asynchronous on `stream` (NULL = the context's stream): the halda_fleets and
+ * halda_fleet_result arrays are device memory; ks (host memory, n_k entries)
+ * is ascending, unique, > 0. Shape limits: L / ks[0] - min_devices + 1 <= 128. */
+int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                       int32_t n_k, halda_fleet_result *out, void *stream);
+
+/* Synchronous variant on HOST arrays (halda_fleets / halda_fleet_result in host
+ * memory; obj_by_k and status may be NULL). */
+int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                            int32_t n_k, halda_fleet_result *out);
+
+/* The lowered batch of the last halda_solve_fleets call (device pointers into ctx
+ * scratch, valid until the next call on ctx): for tests and diagnostics. */
+int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved);
+
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc);
 

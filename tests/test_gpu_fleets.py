@@ -1,0 +1,122 @@
+"""GPU k-sweeps from a device-field table (libhalda halda_solve_fleets): the GPU lowering is
+bit-identical to the host lowering (itself pinned to the reference's arrays by test_lowering), and
+the per-fleet results equal the host-lowered path's and the reference goldens."""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from distilp_amd.common import DeviceProfile
+from distilp_amd.solver import halda_solve_batch
+from distilp_amd.solver._libhalda import HaldaBatchC, HaldaResultC, get_context
+from distilp_amd.solver.fleets import _bind, fleet_table, halda_solve_fleets, solve_table
+from distilp_amd.solver.lower import lower_fleet
+from distilp_amd.synth import synth_fleet
+
+from .helpers import fixture_fleet, synth_devices
+
+pytestmark = pytest.mark.gpu
+
+KS80 = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+
+
+def _hip():
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def _d2h(ptr, count, dtype):
+    out = np.empty(count, dtype)
+    if count:
+        rc = _hip().hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(out.nbytes), 2)
+        assert rc == 0
+    return out
+
+
+def _lowered():
+    ctx = get_context(0)
+    lib = _bind(ctx.lib)
+    b, r = HaldaBatchC(), HaldaResultC()
+    assert lib.halda_last_lowered(ctx.ctx, ctypes.byref(b), ctypes.byref(r)) == 0
+    return b
+
+
+@pytest.mark.parametrize("M,seeds", [(1, range(6)), (3, range(6)), (7, range(4)), (16, range(3)), (64, range(2))])
+def test_gpu_lowering_is_bit_identical(llama_online_model, M, seeds):
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)] for s in seeds]
+    ks = KS80 + [3, 7]
+    ks = sorted(set(ks))
+    solve_table(fleet_table(fleets, llama_online_model), llama_online_model, ks, 0.5)
+    b = _lowered()
+    n = b.n_inst
+    n_cols, n_rows = _d2h(b.n_cols, n, np.int32), _d2h(b.n_rows, n, np.int32)
+    csr_off, col_off, row_off = (_d2h(getattr(b, f), n, np.int64) for f in ("csr_off", "col_off", "row_off"))
+    for fi, devs in enumerate(fleets):
+        fl = lower_fleet(devs, llama_online_model, "4bit")
+        for j, k in enumerate(ks):
+            i = fi * len(ks) + j
+            m = int(n_rows[i])
+            assert (n_cols[i], m) == (fl.n_cols, fl.n_rows)
+            rp = _d2h(b.row_ptr + 4 * int(csr_off[i]), m + 1, np.int32)
+            assert np.array_equal(np.diff(rp), np.diff(fl.row_ptr))
+            cols = _d2h(b.col_idx + 4 * int(rp[0]), int(rp[-1] - rp[0]), np.int32)
+            vals = _d2h(b.val + 8 * int(rp[0]), int(rp[-1] - rp[0]), np.float64)
+            assert np.array_equal(cols, fl.col_idx) and np.array_equal(vals, fl.val), (M, fi, k)
+            c, lb, ub, rlb, rub, integ, W = fl.instance(k)
+            co, ro = int(col_off[i]), int(row_off[i])
+            assert np.array_equal(_d2h(b.c + 8 * co, fl.n_cols, np.float64), c)
+            assert np.array_equal(_d2h(b.col_lb + 8 * co, fl.n_cols, np.float64), lb)
+            assert np.array_equal(_d2h(b.col_ub + 8 * co, fl.n_cols, np.float64), ub)
+            assert np.array_equal(_d2h(b.integrality + co, fl.n_cols, np.uint8), integ)
+            assert np.array_equal(_d2h(b.row_lb + 8 * ro, m, np.float64), rlb)
+            assert np.array_equal(_d2h(b.row_ub + 8 * ro, m, np.float64), rub)
+
+
+@pytest.mark.parametrize("M,seeds", [(2, range(40)), (5, range(20)), (16, range(12)), (64, range(8))])
+def test_fleet_sweep_matches_host_lowered_path(llama_online_model, M, seeds):
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s + 900, M)] for s in seeds]
+    host = halda_solve_batch(fleets, llama_online_model, mip_gap=1e-4, kv_bits="4bit")
+    gpu = halda_solve_fleets(fleets, llama_online_model, mip_gap=1e-4, kv_bits="4bit")
+    for h, g in zip(host, gpu):
+        if h is None:
+            assert g is None
+            continue
+        assert (g.k, g.w, g.n, g.sets) == (h.k, h.w, h.n, h.sets)
+        assert abs(g.obj_value - h.obj_value) <= 1e-12 * max(1.0, abs(h.obj_value))
+
+
+def test_fleet_sweep_matches_reference_goldens(synth_golden, fixtures_golden, llama_online_model):
+    for M in (1, 2, 3, 4, 8, 16, 32, 64):
+        G = synth_golden[M]
+        fleets = [synth_devices(M, f["seed"], f["devices"]) for f in G["fleets"]]
+        out = halda_solve_fleets(fleets, llama_online_model, mip_gap=1e-4, kv_bits="4bit")
+        for r, f in zip(out, G["fleets"]):
+            ref = f["result"]
+            assert (r.k, r.w, r.n, r.sets) == (ref["k"], ref["w"], ref["n"], ref["sets"]), (M, f["seed"])
+            assert abs(r.obj_value - ref["obj_value"]) <= 1e-9 * max(1.0, abs(ref["obj_value"]))
+    for key, fx in fixtures_golden["fixtures"].items():
+        devs, model = fixture_fleet(fx["folder"])
+        r = halda_solve_fleets([devs], model, mip_gap=fx["mip_gap"], kv_bits=fx["kv_bits"])[0]
+        ref = fx["result"]
+        assert (r.k, r.w, r.n, r.sets) == (ref["k"], ref["w"], ref["n"], ref["sets"]), key
+        assert abs(r.obj_value - ref["obj_value"]) <= 1e-9 * max(1.0, abs(ref["obj_value"]))
+
+
+def test_fleet_sweep_per_k_objectives(llama_online_model):
+    """obj_by_k equals the host path's per-k objective; infeasible k -> +inf, status 2."""
+    from distilp_amd.solver._libhalda import STATUS_INFEASIBLE
+    from distilp_amd.solver.batch import assemble
+
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, 12)] for s in range(6)]
+    res = solve_table(fleet_table(fleets, llama_online_model), llama_online_model, KS80, 0.5)
+    lowered = [lower_fleet(d, llama_online_model, "4bit") for d in fleets]
+    batch, refs = assemble(lowered, [KS80] * len(lowered))
+    host = get_context(0).solve(batch)
+    for idx, ref in enumerate(refs):
+        j = KS80.index(ref.k)
+        if host.status[idx] == STATUS_INFEASIBLE:
+            assert res.status[ref.fleet, j] == STATUS_INFEASIBLE and np.isinf(res.obj_by_k[ref.fleet, j])
+            continue
+        x = host.x[ref.col_off:ref.col_off + ref.n_cols]
+        want = lowered[ref.fleet].objective_value(ref.c, x)
+        assert abs(res.obj_by_k[ref.fleet, j] - want) <= 1e-12 * max(1.0, abs(want))
