@@ -1803,7 +1803,9 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_k
 // lowering (distilp_amd/solver/lower.py, itself the reference's
 // solve_fixed_k_milp, halda_p_solver.py:59-338, with dense_common.py:25-230):
 // same row order, same zero-dropping, same FP operation order -> the same CSR
-// and vectors bit for bit.
+// and vectors bit for bit. An instance with W = L / k < M (every device needs a
+// layer: bound-infeasible, 8 of the 9 k at M = 64, L = 80) gets only what the
+// screen settles it from: header, w bounds, c[C] and the equality row's bounds.
 struct LowerDims {
     int mmax, n_k;
     int64_t cols, rows, nnz;  // strides per instance (cols, rows) and per fleet (nnz)
@@ -1857,50 +1859,55 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
     const int iC = 7 * M;
     int rows = 0;
     int64_t nnz = 0;
-    // per-block row emission: lane i emits up to 2 rows of <= 8 entries for device i (chunks of 64)
-    auto emit = [&](int nrow_lane, auto &&row_fn) {
+    // per-block row emission: lane i emits up to 2 rows for device i (chunks of 64). Two passes of the
+    // row function: count the nonzeros, scan, then write the entries straight to the CSR (no private
+    // arrays: dynamically indexed ones would live in scratch).
+    auto emit = [&](auto &&row_fn) {
         for (int i0 = 0; i0 < M; i0 += 64) {
             const int i = i0 + lane;
             const bool act = i < M;
-            int cnt[2] = {0, 0};
-            int cols[2][8];
-            double vals[2][8];
-            double rhs[2] = {0.0, 0.0};
-            int nr = 0;
-            if (act) nr = row_fn(i, cols, vals, rhs, cnt);
-            (void)nrow_lane;
+            int c0 = 0, c1 = 0;
+            double r0 = 0.0, r1 = 0.0;
+            const int nr = act ? row_fn(i, false, c0, c1, r0, r1, int64_t(0), int64_t(0)) : 0;
             int rtot = 0, ntot = 0;
             const int rbase = wave_excl_scan(nr, lane, &rtot);
-            const int nbase = wave_excl_scan(cnt[0] + cnt[1], lane, &ntot);
-            for (int q = 0; q < nr; ++q) {
-                const int r = rows + rbase + q;
-                const int64_t e0 = nnz + nbase + (q ? cnt[0] : 0);
-                O.row_ptr[rp0 + r] = int32_t(nnz0 + e0);
-                for (int k = 0; k < cnt[q]; ++k) {
-                    O.col_idx[nnz0 + e0 + k] = cols[q][k];
-                    O.val[nnz0 + e0 + k] = vals[q][k];
-                }
+            const int nbase = wave_excl_scan(c0 + c1, lane, &ntot);
+            if (nr > 0) {
+                const int64_t e0 = nnz0 + nnz + nbase, e1 = e0 + c0;
+                int w0 = 0, w1 = 0;
+                row_fn(i, true, w0, w1, r0, r1, e0, e1);
+                const int r = rows + rbase;
+                O.row_ptr[rp0 + r] = int32_t(e0);
+                if (nr > 1) O.row_ptr[rp0 + r + 1] = int32_t(e1);
                 for (int j = 0; j < n_k; ++j) {
+                    if (Mo.L / ks[j] < M) continue;  // bound-infeasible: the screen reads only the eq row
                     const int64_t ro = (int64_t(f) * n_k + j) * D.rows;
                     O.row_lb[ro + r] = -kInf;
-                    O.row_ub[ro + r] = rhs[q];
+                    O.row_ub[ro + r] = r0;
+                    if (nr > 1) {
+                        O.row_lb[ro + r + 1] = -kInf;
+                        O.row_ub[ro + r + 1] = r1;
+                    }
                 }
             }
             rows += rtot;
             nnz += ntot;
         }
     };
-    // append (col, val) when val != 0 (scipy builds its CSC from the dense rows)
-    auto put = [](int (&cc)[8], double (&vv)[8], int &n, int col, double v) {
+    // one (col, val) of a row when val != 0 (scipy builds its CSC from the dense rows): counted, or
+    // written at e + n when wr
+    auto put = [&](bool wr, int64_t e, int &n, int col, double v) {
         if (v != 0.0) {
-            cc[n] = col;
-            vv[n] = v;
+            if (wr) {
+                O.col_idx[e + n] = col;
+                O.val[e + n] = v;
+            }
             ++n;
         }
     };
-    // ---- per-device coefficients (lower._device_arrays order)
-    auto coeff = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
-                     double &bcio, double &xi) {
+    // ---- per-device coefficients (lower._device_arrays order); lane i's own device is computed once
+    auto coeff_calc = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
+                          double &bcio, double &xi) {
         const int64_t g = d0 + i;
         const uint8_t fl = F.flags[g];
         const int cls = F.os_class[g];
@@ -1921,64 +1928,85 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         p_v = cls == 2 ? p_b : p_bp;
         cst = xi + F.t_comm[g];
     };
+    double m_alpha = 0, m_b = 0, m_pbp = 0, m_pb = 0, m_pv = 0, m_cst = 0, m_bcio = 0, m_xi = 0;
+    if (lane < M) coeff_calc(lane, m_alpha, m_b, m_pbp, m_pb, m_pv, m_cst, m_bcio, m_xi);
+    auto coeff = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
+                     double &bcio, double &xi) {
+        if (i == lane) {
+            alpha = m_alpha; b = m_b; p_bp = m_pbp; p_b = m_pb; p_v = m_pv; cst = m_cst; bcio = m_bcio; xi = m_xi;
+        } else {
+            coeff_calc(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+        }
+    };
     // 1. link rows n_i - w_i <= 0
-    emit(1, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
-        put(cc[0], vv[0], cn[0], i, -1.0);
-        put(cc[0], vv[0], cn[0], M + i, 1.0);
-        rh[0] = 0.0;
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+        (void)c1; (void)r1; (void)e1;
+        put(wr, e0, c0, i, -1.0);
+        put(wr, e0, c0, M + i, 1.0);
+        r0 = 0.0;
         return 1;
     });
     // 2-4. RAM / Metal capacity rows by set
     for (int set = 1; set <= 3; ++set) {
-        emit(1, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+        emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+            (void)c1; (void)r1; (void)e1;
             const int64_t g = d0 + i;
             if (F.os_class[g] != set) return 0;
             if (set == 2 && !(F.flags[g] & HALDA_DEV_METAL_AVAIL)) return 0;
             double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
             coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
-            put(cc[0], vv[0], cn[0], i, bp);
-            if (set == 3) put(cc[0], vv[0], cn[0], M + i, -bp);
-            put(cc[0], vv[0], cn[0], (1 + set) * M + i, -bp);
-            if (set == 1) rh[0] = double(F.d_avail_ram[g]) - bcio;
-            else if (set == 2) rh[0] = double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
-            else rh[0] = double(F.d_avail_ram[g] + F.swap[g]) - bcio;
+            put(wr, e0, c0, i, bp);
+            if (set == 3) put(wr, e0, c0, M + i, -bp);
+            put(wr, e0, c0, (1 + set) * M + i, -bp);
+            if (set == 1) r0 = double(F.d_avail_ram[g]) - bcio;
+            else if (set == 2) r0 = double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
+            else r0 = double(F.d_avail_ram[g] + F.swap[g]) - bcio;
             return 1;
         });
     }
     // 5. VRAM rows: per device the CUDA row, then the Metal row
-    emit(2, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
         const int64_t g = d0 + i;
         const uint8_t fl = F.flags[g];
-        int q = 0;
-        if (fl & HALDA_DEV_CUDA_OK) {
-            put(cc[q], vv[q], cn[q], M + i, bp);
-            put(cc[q], vv[q], cn[q], 5 * M + i, -bp);
-            rh[q] = double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
-            ++q;
+        const bool cu = fl & HALDA_DEV_CUDA_OK, me = fl & HALDA_DEV_METAL_OK;
+        const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+        const double rc = double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
+        const double rm = double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
+        if (cu) {
+            put(wr, e0, c0, M + i, bp);
+            put(wr, e0, c0, 5 * M + i, -bp);
+            r0 = rc;
         }
-        if (fl & HALDA_DEV_METAL_OK) {
-            const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-            put(cc[q], vv[q], cn[q], M + i, bp);
-            put(cc[q], vv[q], cn[q], 5 * M + i, -bp);
-            rh[q] = double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
-            ++q;
+        if (me) {
+            int &cm = cu ? c1 : c0;
+            const int64_t em = cu ? e1 : e0;
+            put(wr, em, cm, M + i, bp);
+            put(wr, em, cm, 5 * M + i, -bp);
+            (cu ? r1 : r0) = rm;
         }
-        return q;
+        return int(cu) + int(me);
     });
     // 6. cycle rows busy + z - C <= -const ; busy + F - z - C <= -const
-    emit(2, [&](int i, int (&cc)[2][8], double (&vv)[2][8], double (&rh)[2], int (&cn)[2]) {
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
         double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
         coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
-        const double busy[6] = {alpha, b, p_bp, p_b, p_bp, p_v};
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            put(cc[q], vv[q], cn[q], i, q == 0 ? busy[0] : busy[0] + p_bp);
-#pragma unroll
-            for (int blk = 1; blk < 6; ++blk) put(cc[q], vv[q], cn[q], blk * M + i, busy[blk]);
-            put(cc[q], vv[q], cn[q], 6 * M + i, q == 0 ? 1.0 : -1.0);
-            put(cc[q], vv[q], cn[q], iC, -1.0);
-            rh[q] = -cst;
-        }
+        put(wr, e0, c0, i, alpha);
+        put(wr, e1, c1, i, alpha + p_bp);
+        put(wr, e0, c0, M + i, b);
+        put(wr, e1, c1, M + i, b);
+        put(wr, e0, c0, 2 * M + i, p_bp);
+        put(wr, e1, c1, 2 * M + i, p_bp);
+        put(wr, e0, c0, 3 * M + i, p_b);
+        put(wr, e1, c1, 3 * M + i, p_b);
+        put(wr, e0, c0, 4 * M + i, p_bp);
+        put(wr, e1, c1, 4 * M + i, p_bp);
+        put(wr, e0, c0, 5 * M + i, p_v);
+        put(wr, e1, c1, 5 * M + i, p_v);
+        put(wr, e0, c0, 6 * M + i, 1.0);
+        put(wr, e1, c1, 6 * M + i, -1.0);
+        put(wr, e0, c0, iC, -1.0);
+        put(wr, e1, c1, iC, -1.0);
+        r0 = r1 = -cst;
         return 2;
     });
     // 7. equality row sum_i w_i = W (row bounds per k below)
@@ -2008,6 +2036,12 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         for (int j = 0; j < n_k; ++j) {
             const double W = double(Mo.L / ks[j]);
             const int64_t co = (int64_t(f) * n_k + j) * D.cols;
+            if (Mo.L / ks[j] < M) {
+                // W < M = sum lb(w): the screen settles it from the w bounds (and c[C], the eq row)
+                O.col_lb[co + i] = 1.0;
+                O.col_ub[co + i] = W;
+                continue;
+            }
 #pragma unroll
             for (int blk = 0; blk < 6; ++blk) {
                 O.c[co + blk * M + i] = busy[blk];
@@ -2037,27 +2071,45 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         O.col_off[inst] = co;
         O.row_off[inst] = ro;
     }
-    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230)
-    if (lane == 0) {
-        double tsum = 0.0, xsum = 0.0;
-        int hi = -1;
-        for (int i = 0; i < M; ++i) {
-            const int64_t g = d0 + i;
-            tsum += F.t_comm[g];
-            xsum += (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
-            if (hi < 0 && (F.flags[g] & HALDA_DEV_HEAD)) hi = i;
+    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230).
+    // Lane-parallel loads, then the reference's sequential sums over readlane (no serial memory chain).
+    double tsum = 0.0, xsum = 0.0, tail1 = 0.0, tail3 = 0.0;
+    int hi = -1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const double tc = F.t_comm[g];
+        const double xv = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const uint64_t heads = __ballot(i0 + lane < M && (F.flags[g] & HALDA_DEV_HEAD));
+        if (hi < 0 && heads) hi = i0 + __builtin_ctzll(heads);
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q) {
+            tsum += bcast(tc, q);
+            xsum += bcast(xv, q);
+            const int cq = bcast(cls, q);
+            if (cq == 1) tail1 += bcast(tl, q);
         }
+        (void)tail3;
+    }
+    // the M3 part of the tail follows all of M1 (dense_common.py:226: M1 + M3 order)
+    double tail = tail1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q)
+            if (bcast(cls, q) == 3) tail += bcast(tl, q);
+    }
+    if (lane == 0) {
         const int64_t h = d0 + (hi < 0 ? 0 : hi);
         double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
         total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
         total += Mo.b_in / (Mo.V * F.s_disk[h]);
         total += Mo.b_out / F.s_disk[h];
-        double tail = 0.0;
-        for (int set = 1; set <= 3; set += 2)
-            for (int i = 0; i < M; ++i) {
-                const int64_t g = d0 + i;
-                if (F.os_class[g] == set) tail += double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
-            }
         O.offs[3 * f + 0] = tsum;
         O.offs[3 * f + 1] = xsum;
         O.offs[3 * f + 2] = total + tail;
@@ -2101,7 +2153,7 @@ __global__ __launch_bounds__(64) void halda_pick_kernel(halda_batch B, halda_res
             const int N = B.n_cols[inst];
             for (int cc = lane; cc < N; cc += 64) {
                 if (out.x) out.x[inst * xstride + cc] = st == HALDA_STATUS_OPTIMAL ? R.x[co + cc] : 0.0;
-                if (out.c) out.c[inst * xstride + cc] = B.c[co + cc];
+                if (out.c) out.c[inst * xstride + cc] = st == HALDA_STATUS_OPTIMAL ? B.c[co + cc] : 0.0;
             }
         }
     }

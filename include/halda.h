@@ -195,7 +195,10 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
                             int32_t n_k, halda_fleet_result *out);
 
 /* The lowered batch of the last halda_solve_fleets call (device pointers into ctx
- * scratch, valid until the next call on ctx): for tests and diagnostics. */
+ * scratch, valid until the next call on ctx): for tests and diagnostics. An
+ * instance with L / k < M (bound-infeasible) carries only its header, w bounds,
+ * c[C] and equality-row bounds. x / c of halda_fleet_result are 0 for every
+ * instance that is not OPTIMAL. */
 int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved);
 
 /* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
