@@ -234,6 +234,7 @@ def main():
         raise RuntimeError(f"unexpected statuses: {np.unique(st, return_counts=True)}")
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.set_timing(False)  # no per-launch instrumentation events inside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -253,6 +254,7 @@ def main():
         elapsed = float(t.item())
     # per-launch device times (HIP events recorded by libhalda on the kernels' stream around each
     # launch), after the timed region; the dominant kernel is the longest of them
+    ctx.set_timing(True)
     phases = []
     for _ in range(max(3, min(args.steps, 10))):
         step()

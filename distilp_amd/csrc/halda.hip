@@ -1070,9 +1070,12 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 #endif
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
-                                                          int mmax, int r1max, int tab, int tab_kc) {
+                                                          int mmax, int r1max, int tab, int tab_kc,
+                                                          const int *hb_flag, int launch_id, int gated) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
+    // gated: no k > 1 or wide instance in the batch; only k = 1 hand-backs (flagged) can be here
+    if (gated && __hip_atomic_load(hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != launch_id) return;
     const Slice sl = make_slice(mmax, r1max, tab, tab_kc);
     WaveCtx w;
     w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
@@ -1575,14 +1578,18 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
 // One k = 1 instance (lane = device) from decode to x; hands the instance to the
 // general kernel (cls = CLS_GEN) when the fast path does not apply.
 __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w,
-                         unsigned char *scol, unsigned char *sval, const Inst &I, int lane) {
+                         unsigned char *scol, unsigned char *sval, const Inst &I, int lane, int *hb_flag,
+                         int launch_id) {
     HALDA_STAMP(0);
     Dev d = {};
     int sumlo = 0;
     const int fast = decode_k1(B, w, scol, sval, I, lane, d, sumlo);
     HALDA_PSTAMP(1);
     if (fast == 2) {  // another row order / shape: the general kernel (generic decode) takes it
-        if (lane == 0) cls[I.inst] = CLS_GEN;
+        if (lane == 0) {
+            cls[I.inst] = CLS_GEN;
+            *hb_flag = launch_id;  // the general kernel of this launch has work
+        }
         wave_sync();
         return;
     }
@@ -1599,7 +1606,10 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     wave_sync();  // LDS records are rewritten by the next instance
     HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
-        if (lane == 0) cls[I.inst] = CLS_GEN;  // the general kernel (launched next) takes it
+        if (lane == 0) {
+            cls[I.inst] = CLS_GEN;  // the general kernel (launched next) takes it
+            *hb_flag = launch_id;
+        }
         return;
     }
     if (rc == K1_INFEASIBLE) {
@@ -1651,7 +1661,8 @@ __global__ __launch_bounds__(256) void halda_screen_kernel(halda_batch B, halda_
 // k = 1 fast path: persistent 64-thread workgroups (one wave each) over the
 // instances the screen classed CLS_K1; wave b owns instances b + j * gridDim.x.
 __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_kernel(halda_batch B, halda_result Rz,
-                                                                                      uint8_t *cls, int mmax) {
+                                                                                      uint8_t *cls, int mmax,
+                                                                                      int *hb_flag, int launch_id) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
@@ -1682,7 +1693,7 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
             I.Wd = B.row_ub[I.ro + I.m - 1];
             I.W = int(I.Wd);
             I.kc = B.c[I.co + I.iC];
-            solve_k1(B, Rz, cls, w, scol, sval, I, lane);
+            solve_k1(B, Rz, cls, w, scol, sval, I, lane, hb_flag, launch_id);
         }
     }
 }
@@ -1769,7 +1780,8 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
 // fast path's hand-backs, go to halda_solve_kernel (launched next) through cls.
 __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_kernel(halda_batch B, halda_result Rz,
                                                                                        uint8_t *cls, int mmax,
-                                                                                       int r1max, int tab, int tab_kc) {
+                                                                                       int r1max, int tab, int tab_kc,
+                                                                                       int *hb_flag, int launch_id) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     const int64_t inst = blockIdx.x;
@@ -1793,7 +1805,7 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_k
     I.Wd = h.Wd;
     I.W = int(h.Wd);
     I.kc = h.kc;
-    solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane);
+    solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane, hb_flag, launch_id);
 }
 
 // ---------------------------------------------------------------- GPU lowering
@@ -2195,7 +2207,10 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
+    bool timing = true;  // record the per-launch HIP events (halda_set_timing)
     bool two_pass = false;  // HALDA_TWO_PASS=1: separate screen and persistent k = 1 kernels
+    int *hb_flag = nullptr;  // launch id of the last launch with a k = 1 hand-back
+    int launch_id = 0;
     void *scratch = nullptr;  // host-API staging (device)
     void *pinned = nullptr;   // host-API staging (pinned host), one PCIe copy each way
     size_t pinned_bytes = 0;
@@ -2260,30 +2275,32 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         ctx->work_bytes = (n + 255) & ~size_t(255);
     }
     uint8_t *cls = static_cast<uint8_t *>(ctx->work);
-    HIP_TRY(hipEventRecord(ctx->ev0, stream));
+    const int launch_id = ++ctx->launch_id;  // tags this launch's k = 1 hand-backs (no reset needed)
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
     if (!ctx->two_pass) {
         // one wave per instance: screen, then the k = 1 solve for the survivors
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_screen_k1_kernel), lds1, &per_cu));
         hipLaunchKernelGGL(halda_screen_k1_kernel, dim3(unsigned(in.n_inst)), dim3(64), size_t(lds1), stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc));
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc), ctx->hb_flag, launch_id);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->evk, stream));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
     } else {
         // two passes: screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
                            cls, mmax, in.max_R1, int(tab), int(tab_kc));
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->evk, stream));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_kernel), lds1, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
-        hipLaunchKernelGGL(halda_solve_k1_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls, mmax);
+        hipLaunchKernelGGL(halda_solve_k1_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls, mmax,
+                           ctx->hb_flag, launch_id);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ctx->evs, stream));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evs, stream));
     // general kernel: k > 1, fleets wider than kK1MaxM devices, and the k = 1 instances the fast path
     // handed back (rare). Persistent grid = the resident capacity when the batch's shape summary
     // admits k > 1 or wide instances; otherwise only hand-backs can reach it: one wave per CU.
@@ -2294,11 +2311,12 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         const int64_t cap = general_work ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(cap, in.n_inst)));
         hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds), stream, in, out, cls, mmax,
-                           in.max_R1, int(tab), int(tab_kc));
+                           in.max_R1, int(tab), int(tab_kc), static_cast<const int *>(ctx->hb_flag), launch_id,
+                           int(!general_work));
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ctx->ev1, stream));
-    ctx->timed = true;
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, stream));
+    if (ctx->timing) ctx->timed = true;
     return HALDA_OK;
 }
 
@@ -2336,12 +2354,16 @@ int halda_init(int device_ordinal, void **ctx_out) {
     Ctx *c = new Ctx();
     c->device = device_ordinal;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (hipMalloc(&c->hb_flag, 256) != hipSuccess || hipMemset(c->hb_flag, 0, 256) != hipSuccess) {
+        delete c;
+        return fail(HALDA_E_HIP, "hand-back flag allocation failed");
+    }
     const char *tp = std::getenv("HALDA_TWO_PASS");
     c->two_pass = tp && tp[0] == '1';
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess) {
-        delete c;
+        halda_free(c);
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
     *ctx_out = c;
@@ -2355,6 +2377,7 @@ void halda_free(void *ctx) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->work) (void)hipFree(c->work);
+    if (c->hb_flag) (void)hipFree(c->hb_flag);
     if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -2391,6 +2414,14 @@ int halda_last_solve_kernel_ms(void *ctx, double *ms) {
     float f = 0.f;
     HIP_TRY(hipEventElapsedTime(&f, c->evs, c->ev1));
     *ms = f;
+    return HALDA_OK;
+}
+
+int halda_set_timing(void *ctx, int on) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c) return fail(HALDA_E_ARG, "NULL ctx");
+    c->timing = on != 0;
+    if (!c->timing) c->timed = false;
     return HALDA_OK;
 }
 

@@ -76,7 +76,7 @@ class HaldaResultC(ctypes.Structure):
 
 EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
            "halda_last_solve_kernel_ms", "halda_last_phase_ms", "halda_lds_bytes", "halda_last_error", "halda_free",
-           "halda_solve_fleets", "halda_solve_fleets_host", "halda_last_lowered")
+           "halda_solve_fleets", "halda_solve_fleets_host", "halda_last_lowered", "halda_set_timing")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -107,6 +107,8 @@ def load_library(path: Path | str | None = None):
         lib.halda_last_solve_kernel_ms.restype = ctypes.c_int
         lib.halda_last_phase_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.halda_last_phase_ms.restype = ctypes.c_int
+        lib.halda_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.halda_set_timing.restype = ctypes.c_int
         lib.halda_lds_bytes.argtypes = [ctypes.c_int32] * 4
         lib.halda_lds_bytes.restype = ctypes.c_int64
         lib.halda_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
@@ -251,6 +253,10 @@ class HaldaContext:
         if rc != 0:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
+
+    def set_timing(self, on: bool) -> None:
+        """Record (or not) the per-launch HIP events behind last_kernel_ms / last_phase_ms."""
+        self.lib.halda_set_timing(self.ctx, int(bool(on)))
 
     def last_phase_ms(self) -> Dict[str, float]:
         """Device time of each launch of the last solve: screen, k = 1 fast path, general kernel."""

@@ -119,6 +119,10 @@ int halda_last_kernel_ms(void *ctx, double *ms);
 /* Device time of the last solve's general kernel (halda_solve_kernel) alone, in ms. */
 int halda_last_solve_kernel_ms(void *ctx, double *ms);
 
+/* Record the per-launch HIP events the *_ms queries read (on = 1, the default);
+ * off drops four event records per launch from the stream. */
+int halda_set_timing(void *ctx, int on);
+
 /* Device time of the last solve per launch, in ms: ms3[0] the screen + k = 1
  * kernel (halda_screen_k1_kernel; with HALDA_TWO_PASS=1 in the environment the
  * screen kernel alone), ms3[1] 0 (two-pass: the persistent k = 1 kernel),
