@@ -106,6 +106,21 @@ __device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
 __device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
 __device__ inline int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
 
+// Record of lane `src` broadcast to the whole wave (src wave-uniform).
+__device__ inline double bcast(double v, int src) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane(int(uint32_t(u)), src);
+    const uint32_t hi = __builtin_amdgcn_readlane(int(uint32_t(u >> 32)), src);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+__device__ inline int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+
+__device__ inline double wave_sum_f64(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+
 __device__ inline void write_done(const halda_result &R, int inst, int status, int64_t nodes) {
     R.status[inst] = status;
     R.nodes[inst] = nodes;
@@ -944,6 +959,145 @@ __device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I
     }
 }
 
+// k > 1: incremental threshold scan (lane = device, M <= 64). When every leaf
+// is convex on its finite range and its least cycle time H_i(e) is
+// nondecreasing in e, the mask H_i(e) <= T is a cap e_i <= cap_i(T), and the
+// capped problem S(T) is a separable convex allocation with box constraints:
+// an allocation is optimal iff its largest taken increment is no larger than
+// its smallest available one. Raising T past the next candidate value raises
+// ONE device's cap by one, which makes at most one new increment available, so
+// the optimum of the next T is the current one plus at most one exchange (take
+// the new increment, drop the largest taken one when the new one is smaller).
+// The scan thus costs a few wave reductions per candidate T instead of a full
+// DP pass (leaf scan + greedy / tree + backtrack). Candidates are visited in
+// ascending T (a merge of the devices' sorted H rows) with the same pruning as
+// the pass-per-candidate scan: stop once (k-1) T + S(inf) >= best. Returns
+// false (caller runs the general scan) when a leaf is not convex / monotone.
+// On success st0 holds the allocation (table indices e_i).
+__device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, double s_inf, double best0,
+                                    int64_t &nodes) {
+    const int M = I.M, R1 = I.R1, RS = I.RS;
+    const double kc = I.kc;
+    if (M > 64) return false;
+    const bool act = lane < M;
+    const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
+    int lo = R1, hi = -1;
+    bool ok = true;
+    if (act) {
+        double prev = kInf, dprev = -kInf, hprev = -kInf;
+        int cnt = 0;
+        for (int e = 0; e < R1; ++e) {
+            const double g = G[e];
+            if (!(g < kInf)) continue;
+            if (cnt > 0) {
+                const double d = g - prev;
+                ok = ok && hi == e - 1 && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
+                dprev = d;
+            }
+            ok = ok && H[e] >= hprev;
+            hprev = H[e];
+            lo = min(lo, e);
+            hi = e;
+            prev = g;
+            ++cnt;
+        }
+        ok = ok && cnt > 0;
+    }
+    if (wave_or(act && !ok)) return false;
+    const int need_total = (R1 - 1) - wave_sum(act ? lo : 0);
+    if (need_total < 0 || need_total > wave_sum(act ? hi - lo : 0)) return false;
+    // start at T0 = max_i H_i(lo_i): every device can sit at its first allowed e
+    double T = wave_max(act ? H[lo] : -kInf);
+    int cap = lo;
+    if (act)
+        while (cap < hi && H[cap + 1] <= T) ++cap;
+    // optimal capped allocation at T0 (greedy: every cap filled from lo, then the smallest increments)
+    int e = lo;
+    int need = need_total;
+    {
+        int avail = wave_sum(act ? cap - lo : 0);
+        if (avail <= need) {  // take everything allowed (incomplete when avail < need)
+            e = cap;
+            need -= avail;
+        } else {
+            while (need > 0) {  // rounds: the smallest next increment wins and keeps every one beating the runner-up
+                const double nx = act && e < cap ? G[e + 1] - G[e] : kInf;
+                const double bv = wave_min(nx);
+                const int win = wave_imin(nx == bv ? lane : 0x7fffffff);
+                const double rv = lane == win ? kInf : nx;
+                const double m2 = wave_min(rv);
+                const int d2 = wave_imin(rv == m2 ? lane : 0x7fffffff);
+                int t = 0;
+                if (lane == win) {
+                    while (t < need && e < cap) {
+                        const double x = G[e + 1] - G[e];
+                        if (t > 0 && !(x < m2 || (x == m2 && win < d2))) break;
+                        ++e;
+                        ++t;
+                    }
+                }
+                need -= __builtin_amdgcn_readlane(t, win);
+            }
+        }
+    }
+    double S = wave_sum_f64(act ? G[e] : 0.0);
+    double best = best0;
+    int bestE = -1;
+    int64_t events = 0;
+    auto lam_of = [&](double &lam, int &lj) {  // largest taken increment (ties -> highest device)
+        const double li = act && e > lo ? G[e] - G[e - 1] : -kInf;
+        lam = wave_max(li);
+        lj = -wave_imin(li == lam ? -lane : 0x7fffffff);
+    };
+    double lam = -kInf;
+    int lj = -1;
+    if (need == 0) {
+        lam_of(lam, lj);
+        if (kc * T + S < best) {
+            best = kc * T + S;
+            bestE = e;
+        }
+    }
+    while (true) {
+        const double nx0 = act && cap < hi ? H[cap + 1] : kInf;
+        const double Tn = wave_min(nx0);
+        if (!(Tn < kInf) || !(kc * Tn + s_inf < best)) break;
+        while (true) {  // every cap that opens at Tn, lowest device first
+            const double nx = act && cap < hi ? H[cap + 1] : kInf;
+            const int li = wave_imin(nx == Tn ? lane : 0x7fffffff);
+            if (li == 0x7fffffff) break;
+            ++events;
+            const int capo = __builtin_amdgcn_readlane(cap, li), eo = __builtin_amdgcn_readlane(e, li);
+            const double dd = act && cap < hi ? G[cap + 1] - G[cap] : kInf;
+            const double d = bcast(dd, li);  // the unit cap_o -> cap_o + 1 of device li
+            if (lane == li) ++cap;
+            if (eo != capo) continue;  // li is below its old cap: its next unit was already not worth taking
+            if (need > 0) {
+                if (lane == li) ++e;
+                S += d;
+                if (--need == 0) lam_of(lam, lj);
+            } else if (d < lam) {
+                if (lane == li) ++e;
+                if (lane == lj) --e;
+                S += d - lam;
+                lam_of(lam, lj);
+            }
+        }
+        T = Tn;
+        if (need == 0 && kc * T + S < best) {
+            best = kc * T + S;
+            bestE = e;
+        }
+    }
+    nodes += events;
+    if (bestE >= 0 || !(best0 < kInf)) {  // a capped optimum beat the unconstrained allocation's T
+        if (!(best < kInf)) return false;   // nothing feasible found: let the general scan decide
+        if (act) w.st0[lane] = bestE;
+    }
+    wave_sync();
+    return true;
+}
+
 // DP pass; k > 1: ascending threshold scan with bound pruning. One tree_dp call
 // site: phase 0 = unconstrained, 1 = threshold scan, 2 = final re-run. Leaves the
 // chosen e_i in st0; returns false when infeasible.
@@ -975,6 +1129,8 @@ __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &node
             tlo = wave_max(tlo);
             best = kc * hmax + s_inf;
             phase = 1;
+            // convex leaves with monotone cycle times: one exchange per candidate T
+            if (kc_scan_incremental(w, I, lane, s_inf, best, nodes)) return true;
         } else if (st < kInf && kc * T + st < best) {
             best = kc * T + st;
             bestT = T;
@@ -1186,15 +1342,6 @@ __host__ __device__ inline K1Slice make_k1_slice(int mmax) {
     return s;
 }
 
-// Record of lane `src` broadcast to the whole wave (src wave-uniform).
-__device__ inline double bcast(double v, int src) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane(int(uint32_t(u)), src);
-    const uint32_t hi = __builtin_amdgcn_readlane(int(uint32_t(u >> 32)), src);
-    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-}
-__device__ inline int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
-
 __device__ inline Dev bcast_dev(const Dev &d, int src) {
     Dev o;
     o.cw = bcast(d.cw, src); o.cn = bcast(d.cn, src);
@@ -1220,10 +1367,6 @@ __device__ inline double shfl_up1(double v, int lane) {
     return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
 }
 
-__device__ inline double wave_sum_f64(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
 enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
 
