@@ -47,7 +47,40 @@ constexpr double kSlackEps = 1e-9;  // a capacity row counts as met within 1e-9 
 constexpr double kInf = __builtin_huge_val();
 constexpr int kK1MaxM = 64;         // widest fleet the k = 1 fast path takes (lane = device)
 
-enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2 };  // screen verdicts: settled / k = 1 fast path / general kernel
+// screen verdicts: settled / k = 1 fast path / general kernel for k > 1 / general kernel for k = 1
+// (fleets wider than kK1MaxM and the fast path's hand-backs)
+enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3 };
+
+// Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
+// phase boundaries of the solve kernel, read back with halda_debug_stamps().
+#ifdef HALDA_STAMPS
+constexpr int kStampInst = 65536, kStamps = 8;
+__device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
+#define HALDA_STAMP(k)                                                                                  \
+    do {                                                                                                \
+        if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define HALDA_STAMP(k) \
+    do {               \
+    } while (0)
+#endif
+// -DHALDA_STAMPS_DECODE: stamps 1..5 mark the round trips inside decode_k1 instead
+#ifdef HALDA_STAMPS_DECODE
+#define HALDA_DSTAMP(k) HALDA_STAMP(k)
+#define HALDA_PSTAMP(k) do {} while (0)
+#else
+#define HALDA_DSTAMP(k) do {} while (0)
+#define HALDA_PSTAMP(k) HALDA_STAMP(k)
+#endif
+// -DHALDA_STAMPS_DP: stamps 1..5 mark the steps of the general kernel's k > 1 DP pass instead
+#ifdef HALDA_STAMPS_DP
+#define HALDA_KSTAMP(k) HALDA_STAMP(k)
+#define HALDA_GSTAMP(k) do {} while (0)
+#else
+#define HALDA_KSTAMP(k) do {} while (0)
+#define HALDA_GSTAMP(k) HALDA_STAMP(k)
+#endif
 
 // ---------------------------------------------------------------- LDS slice
 // One solve wave = one 64-thread workgroup with its own LDS slice (bytes):
@@ -105,6 +138,16 @@ __device__ inline double wave_max(double v) { return __ockl_wfred_max_f64(v); }
 __device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
 __device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
 __device__ inline int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
+// Lowest / highest lane whose predicate holds (all lanes active), 0x7fffffff / -1 when none: a
+// ballot instead of a second wave reduction for the arg of a min / max.
+__device__ inline int lowest_lane(bool p) {
+    const uint64_t b = __ballot(p);
+    return b ? __builtin_ctzll(b) : 0x7fffffff;
+}
+__device__ inline int highest_lane(bool p) {
+    const uint64_t b = __ballot(p);
+    return b ? 63 - __builtin_clzll(b) : -1;
+}
 
 // Record of lane `src` broadcast to the whole wave (src wave-uniform).
 __device__ inline double bcast(double v, int src) {
@@ -241,7 +284,7 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
             const int R1 = W - sumlo + 1;
             const bool kc = __shfl(cC, g) > 0.0;
             if (R1 > r1max || int64_t(Mg) * odd_stride(R1) > (kc ? tab_kc : tab)) st = HALDA_STATUS_TOO_LARGE;
-            else v = (kc || Mg > kK1MaxM) ? CLS_GEN : CLS_K1;
+            else v = kc ? CLS_GEN : (Mg > kK1MaxM ? CLS_GEN1 : CLS_K1);
         }
         if (lane == g) {
             vstatus = st;
@@ -453,8 +496,10 @@ __device__ inline void load_dev(Dev &d, const halda_batch &B, const WaveCtx &w, 
 struct LeafInfo {
     bool convex;  // every leaf's finite set is an interval and the leaf is convex on it
     bool empty;   // some leaf has no allowed entry (the call is infeasible)
+    bool mono;    // every leaf's H is nondecreasing on its finite set
     int lo_sum;   // sum of the leaves' first allowed e
     int cap;      // sum of (hi - lo)
+    int my_lo, my_hi;  // this lane's leaf range (device i = lane; M <= 64)
 };
 
 // Leaf pre-pass of one DP call (lane = device): finite range [lo, hi] of the
@@ -462,22 +507,26 @@ struct LeafInfo {
 // cost is L-natural convex in (w, n), so G_i (its minimum over n) is convex in w
 // and its threshold sublevel sets are intervals; the check guards the floating
 // point (increments must not decrease by more than 1e-12 relative).
-__device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, int lane) {
-    bool ok = true, empty = false;
-    int lo_sum = 0, cap = 0;
+__device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, int lane,
+                                bool want_mono = false) {
+    bool ok = true, empty = false, mono = true;
+    int lo_sum = 0, cap = 0, my_lo = R1, my_hi = -1;
     for (int i = lane; i < M; i += 64) {
         const double *G = w.G + int64_t(i) * RS, *H = w.H + int64_t(i) * RS;
         int lo = R1, hi = -1, cnt = 0;
-        double prev = kInf, dprev = -kInf;
+        double prev = kInf, dprev = -kInf, hprev = -kInf;
         for (int e = 0; e < R1; ++e) {
             const double g = G[e];
-            const bool in = g < kInf && (!use_T || H[e] <= T);
+            const double h = want_mono || use_T ? H[e] : 0.0;
+            const bool in = g < kInf && (!use_T || h <= T);
             if (in) {
                 if (cnt > 0) {
                     const double d = g - prev;
                     ok = ok && (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
                     dprev = d;
                 }
+                mono = mono && h >= hprev;
+                hprev = h;
                 lo = min(lo, e);
                 hi = e;
                 prev = g;
@@ -488,8 +537,15 @@ __device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool us
         lo_sum += lo;
         cap += hi - lo;
         w.rng[i] = make_int2(lo, hi);
+        if (i == lane) {
+            my_lo = lo;
+            my_hi = hi;
+        }
     }
     LeafInfo li;
+    li.mono = want_mono && !wave_or(!mono);
+    li.my_lo = my_lo;
+    li.my_hi = my_hi;
     li.convex = !wave_or(!ok);
     li.empty = wave_or(empty);
     li.lo_sum = wave_sum(lo_sum);
@@ -711,9 +767,11 @@ __device__ void tree_backtrack(const WaveCtx &w, int M, int R1, int lane) {
 // One DP call: leaf ranges / convexity check, then the greedy exchange (convex
 // leaves, few layers to hand out) or the tree; leaves the chosen e_i in st0 and
 // returns the minimum (+inf when infeasible).
-__device__ double dp_call(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane) {
+__device__ double dp_call(const WaveCtx &w, int M, int R1, int RS, bool use_T, double T, double *buf, int lane,
+                          LeafInfo *li_out = nullptr) {
     if (M > 1) {
-        const LeafInfo li = leaf_ranges(w, M, R1, RS, use_T, T, lane);
+        const LeafInfo li = leaf_ranges(w, M, R1, RS, use_T, T, lane, li_out != nullptr);
+        if (li_out) *li_out = li;
         wave_sync();
         if (li.convex && (R1 - 1) - li.lo_sum <= 48) return greedy_alloc(w, M, R1, RS, li, lane);
         const double v = tree_dp(w, M, R1, RS, use_T, T, buf, lane, li.convex);
@@ -949,7 +1007,23 @@ __device__ inline void table_entry(const Dev &d, const WaveCtx &w, const Inst &I
 
 // Table pass (lane = device): G[i][e] (and H[i][e] for k > 1), w = lb + e, one
 // incremental chain per device (split_step reuses the previous argmin).
+// Fleets of at most 32 devices spread each device's chain over P = 64 / M lanes
+// (each starts its stretch of e with a full split search): the least minimiser
+// n*(w) is the same either way, so G and H are too.
 __device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane) {
+    if (I.M <= 32) {
+        const int P = 64 / I.M, chunk = (I.R1 + P - 1) / P;
+        const int i = lane / P, p = lane - i * P;
+        if (i < I.M) {
+            Dev d;
+            load_dev(d, B, w, I.co, I.M, i, I.Wd);
+            int n = 0;
+            bool have = false;
+            const int e1 = min(I.R1, (p + 1) * chunk);
+            for (int e = p * chunk; e < e1; ++e) table_entry(d, w, I, i, e, n, have);
+        }
+        return;
+    }
     for (int i = lane; i < I.M; i += 64) {
         Dev d;
         load_dev(d, B, w, I.co, I.M, i, I.Wd);
@@ -975,37 +1049,16 @@ __device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I
 // false (caller runs the general scan) when a leaf is not convex / monotone.
 // On success st0 holds the allocation (table indices e_i).
 __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, double s_inf, double best0,
-                                    int64_t &nodes) {
+                                    int64_t &nodes, const LeafInfo &li0) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const double kc = I.kc;
-    if (M > 64) return false;
+    if (M > 64 || M < 2 || !li0.convex || !li0.mono || li0.empty) return false;
+    HALDA_KSTAMP(3);
     const bool act = lane < M;
     const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
-    int lo = R1, hi = -1;
-    bool ok = true;
-    if (act) {
-        double prev = kInf, dprev = -kInf, hprev = -kInf;
-        int cnt = 0;
-        for (int e = 0; e < R1; ++e) {
-            const double g = G[e];
-            if (!(g < kInf)) continue;
-            if (cnt > 0) {
-                const double d = g - prev;
-                ok = ok && hi == e - 1 && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
-                dprev = d;
-            }
-            ok = ok && H[e] >= hprev;
-            hprev = H[e];
-            lo = min(lo, e);
-            hi = e;
-            prev = g;
-            ++cnt;
-        }
-        ok = ok && cnt > 0;
-    }
-    if (wave_or(act && !ok)) return false;
-    const int need_total = (R1 - 1) - wave_sum(act ? lo : 0);
-    if (need_total < 0 || need_total > wave_sum(act ? hi - lo : 0)) return false;
+    const int lo = act ? li0.my_lo : 0, hi = act ? li0.my_hi : -1;
+    const int need_total = (R1 - 1) - li0.lo_sum;
+    if (need_total < 0 || need_total > li0.cap) return false;
     // start at T0 = max_i H_i(lo_i): every device can sit at its first allowed e
     double T = wave_max(act ? H[lo] : -kInf);
     int cap = lo;
@@ -1015,7 +1068,7 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     int e = lo;
     int need = need_total;
     {
-        int avail = wave_sum(act ? cap - lo : 0);
+        const int avail = wave_sum(act ? cap - lo : 0);
         if (avail <= need) {  // take everything allowed (incomplete when avail < need)
             e = cap;
             need -= avail;
@@ -1023,10 +1076,10 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
             while (need > 0) {  // rounds: the smallest next increment wins and keeps every one beating the runner-up
                 const double nx = act && e < cap ? G[e + 1] - G[e] : kInf;
                 const double bv = wave_min(nx);
-                const int win = wave_imin(nx == bv ? lane : 0x7fffffff);
+                const int win = lowest_lane(nx == bv);
                 const double rv = lane == win ? kInf : nx;
                 const double m2 = wave_min(rv);
-                const int d2 = wave_imin(rv == m2 ? lane : 0x7fffffff);
+                const int d2 = lowest_lane(rv == m2);
                 int t = 0;
                 if (lane == win) {
                     while (t < need && e < cap) {
@@ -1041,47 +1094,55 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
         }
     }
     double S = wave_sum_f64(act ? G[e] : 0.0);
+    HALDA_KSTAMP(4);
     double best = best0;
     int bestE = -1;
     int64_t events = 0;
-    auto lam_of = [&](double &lam, int &lj) {  // largest taken increment (ties -> highest device)
-        const double li = act && e > lo ? G[e] - G[e - 1] : -kInf;
-        lam = wave_max(li);
-        lj = -wave_imin(li == lam ? -lane : 0x7fffffff);
-    };
+    // Only "useful" cap openings change the optimum: device i must sit at its cap (e_i == cap_i; a
+    // device below its cap already declined a unit no worse than its next) and the unit its next cap
+    // opens must be needed (allocation incomplete) or beat the largest taken unit lam. lam only
+    // decreases, so a device that is not useful now never becomes useful except the one that just
+    // took a unit; the scan therefore jumps T straight to the next useful opening and costs one
+    // reduction per exchange instead of one per candidate T.
+    double hn = act && cap < hi ? H[cap + 1] : kInf;   // H of this device's next cap
+    double gn = act && cap < hi ? G[cap + 1] - G[cap] : kInf;  // the unit it opens (cap -> cap + 1)
+    double lt = act && e > lo ? G[e] - G[e - 1] : -kInf;  // its last taken unit
     double lam = -kInf;
     int lj = -1;
     if (need == 0) {
-        lam_of(lam, lj);
+        lam = wave_max(lt);
+        lj = highest_lane(lt == lam);
         if (kc * T + S < best) {
             best = kc * T + S;
             bestE = e;
         }
     }
     while (true) {
-        const double nx0 = act && cap < hi ? H[cap + 1] : kInf;
-        const double Tn = wave_min(nx0);
+        const bool useful = act && e == cap && cap < hi && (need > 0 || gn < lam);
+        const double cand = useful ? hn : kInf;
+        const double Tn = wave_min(cand);
         if (!(Tn < kInf) || !(kc * Tn + s_inf < best)) break;
-        while (true) {  // every cap that opens at Tn, lowest device first
-            const double nx = act && cap < hi ? H[cap + 1] : kInf;
-            const int li = wave_imin(nx == Tn ? lane : 0x7fffffff);
-            if (li == 0x7fffffff) break;
-            ++events;
-            const int capo = __builtin_amdgcn_readlane(cap, li), eo = __builtin_amdgcn_readlane(e, li);
-            const double dd = act && cap < hi ? G[cap + 1] - G[cap] : kInf;
-            const double d = bcast(dd, li);  // the unit cap_o -> cap_o + 1 of device li
-            if (lane == li) ++cap;
-            if (eo != capo) continue;  // li is below its old cap: its next unit was already not worth taking
-            if (need > 0) {
-                if (lane == li) ++e;
-                S += d;
-                if (--need == 0) lam_of(lam, lj);
-            } else if (d < lam) {
-                if (lane == li) ++e;
-                if (lane == lj) --e;
-                S += d - lam;
-                lam_of(lam, lj);
-            }
+        const int li = lowest_lane(cand == Tn);
+        ++events;
+        const double d = bcast(gn, li);
+        const bool swap = need == 0;  // else: fill
+        const int ljo = lj;
+        S += swap ? d - lam : d;
+        if (!swap) --need;
+        if (lane == li) {  // li takes the unit its new cap opens
+            cap = e + 1;
+            e = cap;
+            hn = cap < hi ? H[cap + 1] : kInf;
+            gn = cap < hi ? G[cap + 1] - G[cap] : kInf;
+            lt = G[e] - G[e - 1];
+        }
+        if (swap && lane == ljo) {  // ljo gives back its largest taken unit
+            --e;
+            lt = e > lo ? G[e] - G[e - 1] : -kInf;
+        }
+        if (need == 0) {
+            lam = wave_max(lt);
+            lj = highest_lane(lt == lam);
         }
         T = Tn;
         if (need == 0 && kc * T + S < best) {
@@ -1090,8 +1151,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
         }
     }
     nodes += events;
-    if (bestE >= 0 || !(best0 < kInf)) {  // a capped optimum beat the unconstrained allocation's T
-        if (!(best < kInf)) return false;   // nothing feasible found: let the general scan decide
+    HALDA_KSTAMP(5);
+    if (bestE >= 0) {  // a capped optimum beat the unconstrained allocation's own T
         if (act) w.st0[lane] = bestE;
     }
     wave_sync();
@@ -1109,28 +1170,31 @@ __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &node
     bool use_T = false;
     double T = 0.0, s_inf = kInf, best = kInf, bestT = kInf, tprev = -1.0, tlo = 0.0;
     nodes = 0;
+    LeafInfo li0 = {};
     while (true) {
-        const double st = dp_call(w, M, R1, RS, use_T, T, buf, lane);
+        const double st = dp_call(w, M, R1, RS, use_T, T, buf, lane, phase == 0 && kc > 0.0 ? &li0 : nullptr);
         ++nodes;
         if (phase == 2) break;
         if (phase == 0) {
+            HALDA_KSTAMP(1);
             s_inf = st;
             if (!(st < kInf)) return false;
             if (!(kc > 0.0)) break;  // k = 1: the allocation of this pass is final
             double hmax = 0.0;
+            for (int i = lane; i < M; i += 64) hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
+            hmax = wave_max(hmax);
+            best = kc * hmax + s_inf;
+            phase = 1;
+            HALDA_KSTAMP(2);
+            // convex leaves with monotone cycle times: one exchange per candidate T
+            if (kc_scan_incremental(w, I, lane, s_inf, best, nodes, li0)) return true;
             for (int i = lane; i < M; i += 64) {
-                hmax = fmax(hmax, w.H[i * RS + w.st0[i]]);
                 double mn = kInf;
                 for (int e = 0; e < R1; ++e)
                     if (w.G[i * RS + e] < kInf) mn = fmin(mn, w.H[i * RS + e]);
                 tlo = fmax(tlo, mn);  // every assignment has max_i H_i >= max_i min_e H[i][e]
             }
-            hmax = wave_max(hmax);
             tlo = wave_max(tlo);
-            best = kc * hmax + s_inf;
-            phase = 1;
-            // convex leaves with monotone cycle times: one exchange per candidate T
-            if (kc_scan_incremental(w, I, lane, s_inf, best, nodes)) return true;
         } else if (st < kInf && kc * T + st < best) {
             best = kc * T + st;
             bestT = T;
@@ -1198,28 +1262,6 @@ __device__ void output_pass(const halda_batch &B, const halda_result &Rz, const 
     wave_sync();
 }
 
-// Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
-// phase boundaries of the solve kernel, read back with halda_debug_stamps().
-#ifdef HALDA_STAMPS
-constexpr int kStampInst = 65536, kStamps = 8;
-__device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
-#define HALDA_STAMP(k)                                                                                  \
-    do {                                                                                                \
-        if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define HALDA_STAMP(k) \
-    do {               \
-    } while (0)
-#endif
-// -DHALDA_STAMPS_DECODE: stamps 1..5 mark the round trips inside decode_k1 instead
-#ifdef HALDA_STAMPS_DECODE
-#define HALDA_DSTAMP(k) HALDA_STAMP(k)
-#define HALDA_PSTAMP(k) do {} while (0)
-#else
-#define HALDA_DSTAMP(k) do {} while (0)
-#define HALDA_PSTAMP(k) HALDA_STAMP(k)
-#endif
 
 #ifndef HALDA_SOLVE_WAVES_PER_SIMD
 #define HALDA_SOLVE_WAVES_PER_SIMD 2  // occupancy target of the solve kernel (register budget)
@@ -1227,7 +1269,7 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
                                                           int mmax, int r1max, int tab, int tab_kc,
-                                                          const int *hb_flag, int launch_id, int gated) {
+                                                          const int *hb_flag, int launch_id, int gated, int want) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     // gated: no k > 1 or wide instance in the batch; only k = 1 hand-backs (flagged) can be here
@@ -1252,7 +1294,7 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
     const int S = gridDim.x;
     for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
         const int64_t mine = base + int64_t(lane) * S;
-        const bool open = mine < B.n_inst && cls[mine] == CLS_GEN;
+        const bool open = mine < B.n_inst && cls[mine] == want;
         uint64_t todo = __ballot(open);
         while (todo) {
             const int bit = __builtin_ctzll(todo);
@@ -1277,25 +1319,25 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
             I.R1 = I.W - sumlo + 1;
             I.RS = odd_stride(I.R1);
             wave_sync();
-            HALDA_STAMP(1);
+            HALDA_GSTAMP(1);
             bad |= row_pass(B, w, I, lane);
             wave_sync();
-            HALDA_STAMP(2);
+            HALDA_GSTAMP(2);
             bad |= check_rows(w, I.M, lane);
             if (wave_or(bad)) {
                 if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_UNSUPPORTED, 0);
                 continue;
             }
-            HALDA_STAMP(3);
+            HALDA_GSTAMP(3);
             table_pass(B, w, I, lane);
             wave_sync();
-            HALDA_STAMP(4);
+            HALDA_GSTAMP(4);
             int64_t nodes = 0;
             if (!dp_pass(w, I, lane, nodes)) {
                 if (lane == 0) write_done(Rz, I.inst, HALDA_STATUS_INFEASIBLE, nodes);
                 continue;
             }
-            HALDA_STAMP(5);
+            HALDA_GSTAMP(5);
             output_pass(B, Rz, w, I, lane, nodes);
             HALDA_STAMP(6);
         }
@@ -1393,10 +1435,10 @@ __device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &round
         ++rounds;
         const double bv = wave_min(act ? inc : kInf);
         if (!(bv < kInf)) return K1_INFEASIBLE;  // no device can take another layer
-        const int win = wave_imin(act && inc == bv ? lane : 0x7fffffff);
+        const int win = lowest_lane(act && inc == bv);
         const double rv = act && lane != win ? inc : kInf;
         const double m2 = wave_min(rv);
-        const int d2 = wave_imin(act && lane != win && rv == m2 ? lane : 0x7fffffff);
+        const int d2 = lowest_lane(act && lane != win && rv == m2);
         const int ew = bcast(e, win);
         const double gnw = bcast(gn, win), dpw = bcast(dprev, win);
         // the winner takes its next increment bv; lane t evaluates G_win(ew + 2 + t)
@@ -1730,8 +1772,8 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_PSTAMP(1);
     if (fast == 2) {  // another row order / shape: the general kernel (generic decode) takes it
         if (lane == 0) {
-            cls[I.inst] = CLS_GEN;
-            *hb_flag = launch_id;  // the general kernel of this launch has work
+            cls[I.inst] = CLS_GEN1;
+            *hb_flag = launch_id;  // the k = 1 general launch of this batch has work
         }
         wave_sync();
         return;
@@ -1750,7 +1792,7 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
         if (lane == 0) {
-            cls[I.inst] = CLS_GEN;  // the general kernel (launched next) takes it
+            cls[I.inst] = CLS_GEN1;  // the k = 1 general launch (next) takes it
             *hb_flag = launch_id;
         }
         return;
@@ -1897,7 +1939,7 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
             const int R1 = W - sumlo + 1;
             const bool kc = cC > 0.0;
             if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
-            else verdict = (kc || M > kK1MaxM) ? CLS_GEN : CLS_K1;
+            else verdict = kc ? CLS_GEN : (M > kK1MaxM ? CLS_GEN1 : CLS_K1);
         }
     }
     if (lane == 0) {
@@ -2406,7 +2448,8 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     const int64_t tab = std::max<int64_t>(1, in.max_tab > 0 ? int64_t(in.max_tab) + mmax : 0);
     const int64_t tab_kc = in.max_tab_kc > 0 ? int64_t(in.max_tab_kc) + mmax : 0;
     if (tab > (1 << 24) || tab_kc > (1 << 24)) return fail(HALDA_E_ARG, "table summary out of range");
-    const int64_t lds = slice_bytes_for(mmax, in.max_R1, int(tab), int(tab_kc));
+    const int64_t lds = std::max(slice_bytes_for(mmax, in.max_R1, int(tab), 0),
+                                 slice_bytes_for(mmax, in.max_R1, 0, int(tab_kc)));
     if (lds > 160 * 1024)
         return fail(HALDA_E_ARG, "batch needs " + std::to_string(lds) + " B of LDS per solve wave (> 160 KiB)");
     const size_t n = size_t(in.n_inst);
@@ -2444,18 +2487,30 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         HIP_TRY(hipGetLastError());
     }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evs, stream));
-    // general kernel: k > 1, fleets wider than kK1MaxM devices, and the k = 1 instances the fast path
-    // handed back (rare). Persistent grid = the resident capacity when the batch's shape summary
-    // admits k > 1 or wide instances; otherwise only hand-backs can reach it: one wave per CU.
-    {
+    // general kernel, two launches with their own LDS slices: k > 1 instances (tables of the k > 1
+    // shape only), then k = 1 instances of fleets wider than kK1MaxM devices and the fast path's
+    // hand-backs (k = 1 tables). The first runs only when the shape summary admits k > 1 instances;
+    // the second is gated on the hand-back flag unless wide k = 1 fleets are possible.
+    const bool wide = (in.max_cols - 1) / 7 > kK1MaxM;
+    if (tab_kc > 0) {
+        const int64_t lds_kc = slice_bytes_for(mmax, in.max_R1, 0, int(tab_kc));
         int per_cu = 0;
-        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds, &per_cu));
-        const bool general_work = in.max_tab_kc > 0 || (in.max_cols - 1) / 7 > kK1MaxM;
-        const int64_t cap = general_work ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_kc, &per_cu));
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
+        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_kc), stream, in, out, cls, mmax,
+                           in.max_R1, 0, int(tab_kc), static_cast<const int *>(ctx->hb_flag), launch_id, 0,
+                           int(CLS_GEN));
+        HIP_TRY(hipGetLastError());
+    }
+    {
+        const int64_t lds_k1 = slice_bytes_for(mmax, in.max_R1, int(tab), 0);
+        int per_cu = 0;
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_k1, &per_cu));
+        const int64_t cap = wide ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(cap, in.n_inst)));
-        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds), stream, in, out, cls, mmax,
-                           in.max_R1, int(tab), int(tab_kc), static_cast<const int *>(ctx->hb_flag), launch_id,
-                           int(!general_work));
+        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_k1), stream, in, out, cls, mmax,
+                           in.max_R1, int(tab), 0, static_cast<const int *>(ctx->hb_flag), launch_id, int(!wide),
+                           int(CLS_GEN1));
         HIP_TRY(hipGetLastError());
     }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, stream));
@@ -2479,7 +2534,7 @@ int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32
     const int mmax = (max_cols - 1) / 7 + 1;
     const int64_t tab = std::max<int64_t>(1, max_tab > 0 ? int64_t(max_tab) + mmax : 0);
     const int64_t tab_kc = max_tab_kc > 0 ? int64_t(max_tab_kc) + mmax : 0;
-    return slice_bytes_for(mmax, max_R1, int(tab), int(tab_kc));
+    return std::max(slice_bytes_for(mmax, max_R1, int(tab), 0), slice_bytes_for(mmax, max_R1, 0, int(tab_kc)));
 }
 
 int halda_init(int device_ordinal, void **ctx_out) {

@@ -126,7 +126,7 @@ int halda_set_timing(void *ctx, int on);
 /* Device time of the last solve per launch, in ms: ms3[0] the screen + k = 1
  * kernel (halda_screen_k1_kernel; with HALDA_TWO_PASS=1 in the environment the
  * screen kernel alone), ms3[1] 0 (two-pass: the persistent k = 1 kernel),
- * ms3[2] the general kernel. */
+ * ms3[2] the general kernel's launches (k > 1, then k = 1 wide / hand-backs). */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
 /* ------------------------------------------------------------------------
@@ -205,7 +205,7 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
  * instance that is not OPTIMAL. */
 int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved);
 
-/* Bytes of dynamic LDS the solve kernel uses for a batch of this shape (for reporting). */
+/* Bytes of dynamic LDS per wave of the general kernel's larger launch for a batch of this shape. */
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc);
 
 /* Copy the calling thread's last error message into buf. Returns its length. */

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fleets", type=int, default=4096)
     ap.add_argument("--M", type=int, default=64)
+    ap.add_argument("--k", type=int, default=0, help="only instances of this k (0 = all)")
     args = ap.parse_args()
     import bench
     from distilp_amd.solver._libhalda import get_context, load_library
@@ -35,6 +36,8 @@ def main():
     got = lib.halda_debug_stamps(buf, n)
     st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8).astype(np.int64)
     ok = res.status[:n] == 0
+    if args.k:
+        ok &= np.array([r.k == args.k for r in refs[:n]])
     st = st[ok]
     names = ["device", "rows", "check", "tables", "dp", "output"]
     d = np.diff(st[:, :7], axis=1)
