@@ -39,7 +39,7 @@ KS_L80 = [1, 2, 4, 5, 8, 10, 16, 20, 40]
 METRIC = "HALDA MILP instances solved/sec (node), M=64 devs L=80; time-to-optimal"
 
 
-def build_workload(rank: int, fleets: int, M: int):
+def build_workload(rank: int, fleets: int, M: int, ks=None):
     from distilp_amd.common import DeviceProfile, ModelProfileSplit
     from distilp_amd.solver.batch import assemble
     from distilp_amd.solver.lower import lower_fleet
@@ -51,7 +51,7 @@ def build_workload(rank: int, fleets: int, M: int):
     for s in range(rank * fleets, (rank + 1) * fleets):
         devs = [DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)]
         lowered.append(lower_fleet(devs, model, "4bit"))
-    batch, refs = assemble(lowered, [KS_L80] * len(lowered))
+    batch, refs = assemble(lowered, [list(ks or KS_L80)] * len(lowered))
     return model, lowered, batch, refs
 
 
@@ -62,7 +62,7 @@ def algorithmic_bytes(lowered, batch, refs):
     equality row), its header (n_cols, n_rows, 3 offsets), c / col_lb / col_ub (8 B each) and
     integrality (1 B) per column (which contain the w bounds and c[C]), row_lb / row_ub per row,
     x out and the result scalars. A screened instance: its header, the equality row (two row_ptr
-    entries, M col_idx/val, its row bounds), lb/ub of its M w-columns, c[C] and the verdict byte,
+    entries, M col_idx/val, its row bounds), lb of its M w-columns, c[C] and the verdict byte,
     plus the result scalars when the screen settles it (M > W = L/k).
       halda_screen_k1_kernel (default, one wave per instance): settled instances' screen bytes +
         survivors' solve bytes + the verdict byte of every instance;
@@ -73,7 +73,7 @@ def algorithmic_bytes(lowered, batch, refs):
     fleets_solved = set()
     for ref in refs:
         fl = lowered[ref.fleet]
-        scr = hdr + 8 + 12 * fl.M + 16 + 16 * fl.M + 8 + 1
+        scr = hdr + 8 + 12 * fl.M + 16 + 8 * fl.M + 8 + 1
         screen += scr
         if ref.W - fl.M >= 0:
             if ref.fleet not in fleets_solved:
@@ -184,6 +184,7 @@ def main():
     ap.add_argument("--copies", type=int, default=2, help="resident copies of the batch, used in turn")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ks", type=str, default="", help="diagnostic: comma-separated k-candidates instead of C3's")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     args = ap.parse_args()
     if args.cpu_baseline_child:
@@ -208,7 +209,8 @@ def main():
     from distilp_amd.solver._libhalda import get_context
 
     t_setup = time.perf_counter()
-    model, lowered, batch, refs = build_workload(rank, args.fleets, args.M)
+    ks = [int(k) for k in args.ks.split(",")] if args.ks else None
+    model, lowered, batch, refs = build_workload(rank, args.fleets, args.M, ks)
     # args.copies resident copies of the batch, used in turn: the bytes one step reads (~221 MB at C3)
     # times the copies exceed the 256 MiB Infinity Cache, so every step reads its inputs from HBM
     copies = [to_device(batch, torch, dev) for _ in range(args.copies)]

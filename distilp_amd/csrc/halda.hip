@@ -176,7 +176,7 @@ __host__ __device__ inline int odd_stride(int r1) { return r1 | 1; }
 
 // ---------------------------------------------------------------- screen
 // One wave screens kScreenPer consecutive instances. Settles everything
-// decidable from the equality row and the w bounds (non-HALDA shape, bound
+// decidable from the equality row and the w lower bounds (non-HALDA shape, bound
 // infeasibility such as M > W = L/k) and flags the rest for the solve kernel
 // (class 1: c[C] == 0, class 2: c[C] > 0). The loads of all its instances are
 // issued together: headers (lane g = instance g), then equality-row extents and
@@ -218,15 +218,14 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     const int eqs0 = rp[ma - 1], eqe0 = rp[ma];
     const double Wd0 = B.row_ub[ro0 + ma - 1], Wl0 = B.row_lb[ro0 + ma - 1];
     const double cC0 = B.c[co0 + 7 * int64_t(max(M, 0))];
-    double lbv[kScreenPer], ubv[kScreenPer];
+    double lbv[kScreenPer];
     int Mg_[kScreenPer];
 #pragma unroll
     for (int g = 0; g < kScreenPer; ++g) {
         const int Mg = __shfl(M, g);
         const int64_t cg = shfl64(co0, g);
         const int64_t idx = cg + (lane < Mg ? lane : 0);
-        lbv[g] = B.col_lb[idx];
-        ubv[g] = B.col_ub[idx];
+        lbv[g] = B.col_lb[idx];  // w upper bounds are left to the solve
         Mg_[g] = Mg;
     }
     const bool live = own && !status;
@@ -250,10 +249,7 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
         const double v0 = open ? B.val[idx] : 1.0;
         cv[g] = in ? c0 : lane;
         vv[g] = in ? v0 : 1.0;
-        if (!in) {
-            lbv[g] = 0.0;
-            ubv[g] = 0.0;
-        }
+        if (!in) lbv[g] = 0.0;
     }
     int verdict = CLS_DONE, vstatus = status;  // lane g: outcome of instance g
 #pragma unroll
@@ -265,14 +261,14 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
         const int64_t cg = shfl64(co, g);
         const double Wg = __shfl(Wd, g);
         int bad = 0, infeas = 0, sumlo = 0;
-        auto one = [&](int i, int col, double v, double lb, double ub) {
+        auto one = [&](int i, int col, double v, double lb) {
             bad |= col != i || v != 1.0;
-            const int wlo = int(ceil(lb)), whi = int(floor(fmin(ub, Wg)));
-            infeas |= wlo > whi || lb < 0.0;
+            const int wlo = int(ceil(lb));
+            infeas |= wlo > int(Wg) || lb < 0.0;
             sumlo += wlo;
         };
-        if (lane < Mg) one(lane, cv[g], vv[g], lbv[g], ubv[g]);
-        for (int i = lane + 64; i < Mg; i += 64) one(i, B.col_idx[eg + i], B.val[eg + i], B.col_lb[cg + i], B.col_ub[cg + i]);
+        if (lane < Mg) one(lane, cv[g], vv[g], lbv[g]);
+        for (int i = lane + 64; i < Mg; i += 64) one(i, B.col_idx[eg + i], B.val[eg + i], B.col_lb[cg + i]);
         bad = wave_or(bad | (infeas << 1));
         sumlo = wave_sum(sumlo);
         const int W = int(Wg);
@@ -1884,7 +1880,8 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
 }
 
 // Screen of ONE instance by one wave (lane = device): the same verdicts as
-// screen_group. Returns the class; settles (and writes) everything but CLS_K1 /
+// screen_group (neither reads the w upper bounds: a device whose w range is
+// empty makes the solve report the instance infeasible). Returns the class; settles (and writes) everything but CLS_K1 /
 // CLS_GEN. Uniform header values are returned for the solve.
 struct Head {
     int N, m, M;
@@ -1910,7 +1907,7 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
     const double Wd = B.row_ub[h.ro + ma - 1], Wl = B.row_lb[h.ro + ma - 1];
     const double cC = B.c[h.co + 7 * int64_t(M)];
     const int li = lane < M ? lane : 0;
-    double lb = B.col_lb[h.co + li], ub = B.col_ub[h.co + li];
+    const double lb = B.col_lb[h.co + li];  // w upper bounds are left to the solve (decode / tables)
     h.Wd = Wd;
     h.kc = cC;
     if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
@@ -1921,14 +1918,14 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
         const int c0 = B.col_idx[eqs + li];
         const double v0 = B.val[eqs + li];
         int bad = 0, infeas = 0, sumlo = 0;
-        auto one = [&](int i, int col, double v, double l, double u) {
+        auto one = [&](int i, int col, double v, double l) {
             bad |= col != i || v != 1.0;
-            const int wlo = int(ceil(l)), whi = int(floor(fmin(u, Wd)));
-            infeas |= wlo > whi || l < 0.0;
+            const int wlo = int(ceil(l));
+            infeas |= wlo > int(Wd) || l < 0.0;
             sumlo += wlo;
         };
-        if (lane < M) one(lane, c0, v0, lb, ub);
-        for (int i = lane + 64; i < M; i += 64) one(i, B.col_idx[eqs + i], B.val[eqs + i], B.col_lb[h.co + i], B.col_ub[h.co + i]);
+        if (lane < M) one(lane, c0, v0, lb);
+        for (int i = lane + 64; i < M; i += 64) one(i, B.col_idx[eqs + i], B.val[eqs + i], B.col_lb[h.co + i]);
         bad = wave_or(bad | (infeas << 1));
         sumlo = wave_sum(sumlo);
         const int W = int(Wd);

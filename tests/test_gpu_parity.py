@@ -250,3 +250,71 @@ def test_row_order_does_not_matter(llama_online_model, M, seed):
     res = get_context(0).solve(shuffled)
     assert np.array_equal(res.status, base.status)
     assert np.array_equal(res.x, base.x)
+
+
+@pytest.mark.parametrize("M,seed,how", [(3, 0, "coef"), (64, 1, "coef"), (16, 2, "cols"), (6, 3, "hand_back")])
+def test_bad_equality_row_is_rejected(llama_online_model, M, seed, how):
+    """The equality row must read sum_i w_i = W. The fused k = 1 screen defers that check to the
+    k = 1 decode; the general kernel repeats it for instances handed back to it. A corrupted row
+    is UNSUPPORTED on every path (k = 1 fast path, k > 1, hand-back)."""
+    from distilp_amd.common import DeviceProfile
+
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(seed, M)]
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    batch, refs = assemble([fl], [[1, 2]])
+    batch.col_idx, batch.val, batch.col_lb = batch.col_idx.copy(), batch.val.copy(), batch.col_lb.copy()
+    seen = set()  # instances of one fleet may share their CSR
+    for j, ref in enumerate(refs):
+        m = int(batch.n_rows[j])
+        rp = batch.row_ptr[batch.csr_off[j]:]
+        eq = int(rp[m - 1])
+        if eq in seen:
+            continue
+        seen.add(eq)
+        if how == "cols":
+            batch.col_idx[eq], batch.col_idx[eq + 1] = batch.col_idx[eq + 1], batch.col_idx[eq]
+        else:
+            batch.val[eq + 1] = 2.0
+    for ref in refs:
+        if how == "hand_back":
+            p = mo.lower_dense(devs, llama_online_model, ref.k, 0.5)
+            i = [d for d in range(M) if p["ub"][M + d] > 0][0]
+            batch.col_lb[ref.col_off + M + i] = 3.0
+    res = get_context(0).solve(batch)
+    assert list(res.status) == [-1, -1], (how, list(res.status))
+
+
+@pytest.mark.parametrize("M,seed,case", [(5, 0, "empty"), (64, 1, "empty"), (6, 2, "fixed"), (64, 3, "fixed"),
+                                         (16, 4, "capped")])
+def test_w_upper_bounds_are_honoured(llama_online_model, M, seed, case):
+    """The screen reads only the w lower bounds; the w upper bounds are the solve's business. A
+    device with an empty w range (lb 3 > ub 2) makes every k infeasible; a fixed w (lb = ub) or a
+    tight cap must give the exact oracle's optimum. k = 1 (fast path) and k = 2 (general kernel)."""
+    from distilp_amd.common import DeviceProfile
+
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(seed, M)]
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    ks = [1, 2]
+    batch, refs = assemble([fl], [ks])
+    batch.col_lb, batch.col_ub = batch.col_lb.copy(), batch.col_ub.copy()
+    lo, hi = {"empty": (3.0, 2.0), "fixed": (1.0, 1.0), "capped": (1.0, 2.0)}[case]  # lb never below the lowering's (shape summary)
+    probs = []
+    for ref in refs:
+        p = mo.lower_dense(devs, llama_online_model, ref.k, 0.5)
+        p["lb"], p["ub"] = p["lb"].copy(), p["ub"].copy()
+        for i in (0, M // 2):
+            batch.col_lb[ref.col_off + i], batch.col_ub[ref.col_off + i] = lo, hi
+            p["lb"][i], p["ub"][i] = lo, hi
+        probs.append(p)
+    res = get_context(0).solve(batch)
+    for j, (ref, p) in enumerate(zip(refs, probs)):
+        st, xo, b1, b2, _ = mo.exact_solve(p)
+        if st == 2:
+            assert res.status[j] == STATUS_INFEASIBLE, (case, ref.k, res.status[j])
+            continue
+        assert res.status[j] == STATUS_OPTIMAL, (case, ref.k, res.status[j])
+        x = res.x[ref.col_off:ref.col_off + ref.n_cols]
+        assert _obj_close(float(res.obj_lin[j]), b1)
+        assert lo <= x[0] <= hi and lo <= x[M // 2] <= hi
+        if mo.uniqueness_margin_ok(b1, b2):
+            assert np.array_equal(x[:2 * M], xo[:2 * M])
