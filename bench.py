@@ -64,10 +64,10 @@ def algorithmic_bytes(lowered, batch, refs):
     x out and the result scalars. A screened instance: its header, the equality row (two row_ptr
     entries, M col_idx/val, its row bounds), lb of its M w-columns, c[C] and the verdict byte,
     plus the result scalars when the screen settles it (M > W = L/k).
-      halda_screen_k1_kernel (default, one wave per instance): settled instances' screen bytes +
-        survivors' solve bytes + the verdict byte of every instance;
-      halda_screen_kernel + halda_solve_k1_kernel (HALDA_TWO_PASS=1): every instance's screen
-        bytes, then the survivors' solve bytes."""
+      halda_screen_kernel + halda_solve_k1_kernel (default): every instance's screen bytes, then
+        the survivors' solve bytes;
+      halda_screen_k1_kernel (HALDA_TWO_PASS=0, one wave per instance): settled instances' screen
+        bytes + survivors' solve bytes + the verdict byte of every instance."""
     hdr, res = 4 + 4 + 8 + 8 + 8, 4 + 8 + 8 + 8 + 8
     solve, screen, fused = 0, 0, 0
     fleets_solved = set()

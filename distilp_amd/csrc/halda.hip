@@ -54,13 +54,22 @@ enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3 };
 // Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
 // phase boundaries of the solve kernel, read back with halda_debug_stamps().
 #ifdef HALDA_STAMPS
-constexpr int kStampInst = 65536, kStamps = 8;
+constexpr int kStampInst = 65536, kStamps = 10;
 __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 #define HALDA_STAMP(k)                                                                                  \
     do {                                                                                                \
         if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// slots 7..9 of the fused kernel's waves: shader clock at wave start, constant-rate
+// (100 MHz) clock at wave start and at wave end
+#define HALDA_WSTAMP(slot, v)                                                                           \
+    do {                                                                                                \
+        if (lane == 0 && inst < kStampInst) g_halda_stamps[inst * kStamps + (slot)] = (v);              \
+    } while (0)
 #else
+#define HALDA_WSTAMP(slot, v) \
+    do {                      \
+    } while (0)
 #define HALDA_STAMP(k) \
     do {               \
     } while (0)
@@ -182,7 +191,10 @@ __host__ __device__ inline int odd_stride(int r1) { return r1 | 1; }
 // issued together: headers (lane g = instance g), then equality-row extents and
 // bounds (lane g), then per instance the equality row and w bounds (lane =
 // device), so a wave spends three memory round trips on kScreenPer instances.
-constexpr int kScreenPer = 8;
+#ifndef HALDA_SCREEN_PER
+#define HALDA_SCREEN_PER 8
+#endif
+constexpr int kScreenPer = HALDA_SCREEN_PER;
 
 __device__ inline int64_t shfl64(int64_t v, int src) {
     const int lo = __shfl(int(uint32_t(uint64_t(v))), src), hi = __shfl(int(uint32_t(uint64_t(v) >> 32)), src);
@@ -1955,6 +1967,15 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
     return verdict;
 }
 
+// XCD-aware block -> instance map (bijective for any grid): blocks are dealt round-robin
+// over the 8 XCDs (observed placement, speed only), so block b works on instance
+// (b % 8) * ~(n / 8) + b / 8 -- each XCD walks one contiguous range of instances in
+// order, and the instances of one fleet (adjacent, sharing their CSR) meet in one L2.
+__device__ inline int64_t xcd_swizzle(int64_t b, int64_t n) {
+    const int64_t x = b % 8, q = n / 8, r = n % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // Screen + k = 1 fast path, one wave per instance: a settled instance's wave
 // exits after three round trips, so the hardware dispatcher refills its slot at
 // once and the (fewer, longer) solves stay evenly spread over the chip whatever
@@ -1963,12 +1984,18 @@ __device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, u
 __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_kernel(halda_batch B, halda_result Rz,
                                                                                        uint8_t *cls, int mmax,
                                                                                        int r1max, int tab, int tab_kc,
-                                                                                       int *hb_flag, int launch_id) {
+                                                                                       int *hb_flag, int launch_id,
+                                                                                       int swz) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
-    const int64_t inst = blockIdx.x;
+    const int64_t inst = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : int64_t(blockIdx.x);
+    HALDA_WSTAMP(7, __builtin_amdgcn_s_memtime());
+    HALDA_WSTAMP(8, __builtin_amdgcn_s_memrealtime());
     Head h;
-    if (screen_one(B, Rz, cls, inst, lane, mmax, r1max, tab, tab_kc, h) != CLS_K1) return;
+    if (screen_one(B, Rz, cls, inst, lane, mmax, r1max, tab, tab_kc, h) != CLS_K1) {
+        HALDA_WSTAMP(9, __builtin_amdgcn_s_memrealtime());
+        return;
+    }
     const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
     WaveCtx w = {};
     w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
@@ -1988,6 +2015,7 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_k
     I.W = int(h.Wd);
     I.kc = h.kc;
     solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane, hb_flag, launch_id);
+    HALDA_WSTAMP(9, __builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------- GPU lowering
@@ -2390,7 +2418,8 @@ struct Ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
     bool timing = true;  // record the per-launch HIP events (halda_set_timing)
-    bool two_pass = false;  // HALDA_TWO_PASS=1: separate screen and persistent k = 1 kernels
+    bool two_pass = true;  // HALDA_TWO_PASS=0: the fused one-wave-per-instance screen + k = 1 kernel
+    bool xcd_swizzle = true;  // HALDA_XCD_SWIZZLE=0: block b works on instance b
     int *hb_flag = nullptr;  // launch id of the last launch with a k = 1 hand-back
     int launch_id = 0;
     void *scratch = nullptr;  // host-API staging (device)
@@ -2466,7 +2495,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_screen_k1_kernel), lds1, &per_cu));
         hipLaunchKernelGGL(halda_screen_k1_kernel, dim3(unsigned(in.n_inst)), dim3(64), size_t(lds1), stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc), ctx->hb_flag, launch_id);
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc), ctx->hb_flag, launch_id, int(ctx->xcd_swizzle));
         HIP_TRY(hipGetLastError());
         if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
     } else {
@@ -2554,7 +2583,9 @@ int halda_init(int device_ordinal, void **ctx_out) {
         return fail(HALDA_E_HIP, "hand-back flag allocation failed");
     }
     const char *tp = std::getenv("HALDA_TWO_PASS");
-    c->two_pass = tp && tp[0] == '1';
+    c->two_pass = !(tp && tp[0] == '0');
+    const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
+    c->xcd_swizzle = !(xs && xs[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess) {

@@ -77,6 +77,35 @@ def main(R):
                    "WRITE_SIZE taken as bytes. Largest launch per kernel = the C3 batch.")
     (dst / f"{R}_pmc.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
+    mem = mem_counters(src)
+    if mem:
+        (dst / f"{R}_pmc_mem.json").write_text(json.dumps(mem, indent=1))
+
+
+def mem_counters(src):
+    """profiles/run_pmc_mem.sh passes: per kernel, the counters of its largest (C3) launch."""
+    out = {}
+    for p in ("pmc_ta", "pmc_tcp", "pmc_tcc", "pmc_tlb"):
+        f = src / p / "run_counter_collection.csv"
+        if not f.exists():
+            continue
+        d = defaultdict(lambda: defaultdict(list))
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if "halda" in k:
+                d[k][r["Counter_Name"]].append((int(r.get("Grid_Size", 0) or 0), float(r["Counter_Value"])))
+        for k, cs in d.items():
+            for c, v in cs.items():
+                g = max(x[0] for x in v)
+                out.setdefault(k, {})[c] = statistics.median(x[1] for x in v if x[0] == g)
+    for k, c in out.items():
+        if c.get("TCP_TCC_READ_REQ_sum"):
+            c["derived_l1_l2_read_latency_cycles"] = c.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / c["TCP_TCC_READ_REQ_sum"]
+        if c.get("TCC_REQ_sum"):
+            c["derived_l2_hit_rate"] = c.get("TCC_HIT_sum", 0.0) / c["TCC_REQ_sum"]
+        if c.get("SQ_WAVE_CYCLES"):
+            c["derived_wait_any_share"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+    return out
 
 
 if __name__ == "__main__":
