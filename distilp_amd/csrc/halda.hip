@@ -561,6 +561,25 @@ __device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool us
     return li;
 }
 
+// Run of the greedy round's winner over its table row G: increment 0 (its
+// smallest, e0 -> e0 + 1) is taken, and increment t (e0 + t -> e0 + t + 1)
+// follows while each of 1..t still beats the runner-up's m2 (ties go to the lower
+// device index: win_first = winner < runner-up), at most min(need, hi - e0).
+// Lane t evaluates increment t, so a run of up to 64 costs one LDS round trip
+// and a ballot instead of one dependent LDS round trip per increment; longer
+// runs continue in the next round (the winner is then the same device).
+// Returns the (wave-uniform) run length.
+__device__ inline int take_run(const double *G, int e0, int hi, int need, double m2, bool win_first, int lane) {
+    const int lim = min(need, hi - e0);
+    bool fail = true;
+    if (lane >= 1 && lane < lim) {
+        const double x = G[e0 + lane + 1] - G[e0 + lane];
+        fail = !(x < m2 || (x == m2 && win_first));
+    }
+    const uint64_t nb = __ballot(lane >= 1 && fail);
+    return min(nb ? int(__builtin_ctzll(nb)) : 64, lim);
+}
+
 // Separable convex allocation by the greedy exchange: start every device at its
 // first allowed e, then hand out the remaining R - sum(lo) layers one at a time
 // to the device whose next increment G_i[e+1] - G_i[e] is smallest (ties ->
@@ -594,21 +613,14 @@ __device__ double greedy_alloc(const WaveCtx &w, int M, int R1, int RS, const Le
         const int ri = lane == wl ? si : bi;
         const double m2 = wave_min(rv);
         const int d2 = wave_imin(rv == m2 ? ri : 0x7fffffff);
-        int t = 0;
+        const int t = take_run(w.G + int64_t(win) * RS, w.st0[win], w.rng[win].y, need, m2, win < d2, lane);
         if (lane == wl) {
-            int e = w.st0[win];
-            const int hi = w.rng[win].y;
+            const int e = w.st0[win] + t, hi = w.rng[win].y;
             const double *G = w.G + int64_t(win) * RS;
-            while (t < need && e < hi) {
-                const double x = G[e + 1] - G[e];
-                if (!(x < m2 || (x == m2 && win < d2))) break;
-                ++e;
-                ++t;
-            }
             w.st0[win] = e;
             w.inc[win] = e < hi ? G[e + 1] - G[e] : kInf;
         }
-        need -= __builtin_amdgcn_readlane(t, wl);
+        need -= t;
         wave_sync();
     }
     double S = 0.0;
@@ -1088,16 +1100,10 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
                 const double rv = lane == win ? kInf : nx;
                 const double m2 = wave_min(rv);
                 const int d2 = lowest_lane(rv == m2);
-                int t = 0;
-                if (lane == win) {
-                    while (t < need && e < cap) {
-                        const double x = G[e + 1] - G[e];
-                        if (t > 0 && !(x < m2 || (x == m2 && win < d2))) break;
-                        ++e;
-                        ++t;
-                    }
-                }
-                need -= __builtin_amdgcn_readlane(t, win);
+                const int t = take_run(w.G + int64_t(win) * RS, bcast(e, win), bcast(cap, win), need, m2, win < d2,
+                                       lane);
+                if (lane == win) e += t;
+                need -= t;
             }
         }
     }

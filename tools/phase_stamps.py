@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--fleets", type=int, default=4096)
     ap.add_argument("--M", type=int, default=64)
     ap.add_argument("--k", type=int, default=0, help="only instances of this k (0 = all)")
+    ap.add_argument("--dp", action="store_true", help="library built with -DHALDA_STAMPS_DP (stamps 1..5 inside dp_pass)")
     args = ap.parse_args()
     import bench
     from distilp_amd.solver._libhalda import get_context, load_library
@@ -31,15 +32,18 @@ def main():
         res = ctx.solve(batch)
     lib = load_library()
     n = min(batch.n_inst, 65536)
-    buf = (ctypes.c_ulonglong * (8 * n))()
+    K = 10  # kStamps in halda.hip
+    buf = (ctypes.c_ulonglong * (K * n))()
     lib.halda_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     got = lib.halda_debug_stamps(buf, n)
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8).astype(np.int64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(n, K).astype(np.int64)
     ok = res.status[:n] == 0
     if args.k:
         ok &= np.array([r.k == args.k for r in refs[:n]])
     st = st[ok]
     names = ["device", "rows", "check", "tables", "dp", "output"]
+    if args.dp:  # 0 start, 1 phase-0 DP call, 2 hmax, 3 scan entry, 4 scan's first allocation, 5 scan done, 6 output done
+        names = ["decode+tables+dp0", "hmax", "scan setup", "scan alloc0", "scan events", "output"]
     d = np.diff(st[:, :7], axis=1)
     d[:, 2] = st[:, 3] - st[:, 2]
     tot = st[:, 6] - st[:, 0]
