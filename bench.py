@@ -115,7 +115,7 @@ def cpu_baseline_child(budget_s: float, M: int) -> None:
 
     model = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
     tpl = load_templates()
-    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)] for s in range(64)]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)] for s in range(512)]
     t0 = time.perf_counter()
     n_inst = n_fleets = 0
     while time.perf_counter() - t0 < budget_s and n_fleets < len(fleets):
