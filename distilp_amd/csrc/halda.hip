@@ -48,8 +48,9 @@ constexpr double kInf = __builtin_huge_val();
 constexpr int kK1MaxM = 64;         // widest fleet the k = 1 fast path takes (lane = device)
 
 // screen verdicts: settled / k = 1 fast path / general kernel for k > 1 / general kernel for k = 1
-// (fleets wider than kK1MaxM and the fast path's hand-backs)
-enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3 };
+// (fleets wider than kK1MaxM and the fast path's hand-backs) / general kernel on global-memory tables
+// (set by the LDS general launches for instances beyond their slice)
+enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3, CLS_BIG = 4 };
 
 // Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
 // phase boundaries of the solve kernel, read back with halda_debug_stamps().
@@ -103,7 +104,7 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 //   G      [i][e] table, row stride RS (odd), leaves of the DP tree; k = 1 reduces in place
 //   H      [i][e] least cycle time (k > 1 only)
 //   work   DP tree levels when the leaves must survive (k > 1 threshold scan)
-//   split  DP tree argmin (uint8 e of the left subtree), ~M * (R + 1) bytes
+//   split  DP tree argmin (uint16 e of the left subtree), ~2 M (R + 1) bytes
 struct Slice {
     int64_t rows, cyc, cost, cnt, st0, st1, rng, inc, G, H, work, split, total;
 };
@@ -126,7 +127,7 @@ __host__ __device__ inline Slice make_slice(int mmax, int r1max, int tab, int ta
     s.G = o;     o = align16(o + tmax * 8);
     s.H = o;     o = align16(o + int64_t(tab_kc) * 8);
     s.work = o;  o = align16(o + (tab_kc > 0 ? (int64_t(tab_kc) / 2 + 2 * int64_t(r1max) + 2) * 8 : 0));
-    s.split = o; o = align16(o + (int64_t(mmax) + 12) * r1max);
+    s.split = o; o = align16(o + (int64_t(mmax) + 12) * r1max * 2);
     s.total = o;
     return s;
 }
@@ -454,7 +455,7 @@ struct WaveCtx {
     int2 *rng;     // [slot] finite range of a DP-tree node (merge path)
     double *inc;   // [i] next increment of device i (greedy exchange)
     double *G, *H, *work;
-    uint8_t *split;
+    uint16_t *split;
 };
 
 // Device record: costs / decoded rows from LDS, integer bounds from the batch.
@@ -646,12 +647,17 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
     }
     int n = M, l = 0, soff = 0;
     const int npp = R1 <= 64 ? 64 / R1 : 1;  // output nodes per pass
+    // R1 > 64: one node per pass, 128 states (two per lane) per chunk. Node p's output overwrites its
+    // left child in place, and state r reads the left child only at e <= r, so the chunks run from
+    // the highest states down: a chunk never reads what an earlier (higher) chunk wrote.
+    const int nch = R1 <= 64 ? 1 : (R1 + 127) >> 7;
     while (n > 1) {
         const int nout = (n + 1) >> 1;
         ++l;
         const double *src = l == 1 ? w.G : buf;
         const int sh = l == 1 ? 0 : l - 2;  // slot shift of this level's inputs
-        for (int p0 = 0; p0 < nout; p0 += npp) {
+        for (int q = 0; q < ((nout + npp - 1) / npp) * nch; ++q) {
+            const int p0 = (q / nch) * npp, r0 = (nch - 1 - q % nch) << 7;
             // each lane: one (node, r) task, or two states of one node when R1 > 64
             double best[2] = {kInf, kInf};
             int be[2] = {0, 0}, pp[2] = {-1, -1}, rr[2] = {0, 0};
@@ -666,7 +672,7 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
                     if (t > 0 || k >= npp || p >= nout) continue;
                 } else {
                     p = p0;
-                    r = lane + 64 * t;
+                    r = r0 + lane + 64 * t;
                     if (r >= R1) continue;
                 }
                 pp[t] = p;
@@ -732,7 +738,7 @@ __device__ double tree_dp(const WaveCtx &w, int M, int R1, int RS, bool use_T, d
                 if (pp[t] >= 0) {
                     const int slot = pp[t] << (l - 1);
                     buf[int64_t(slot) * RS + rr[t]] = best[t];
-                    w.split[soff + pp[t] * R1 + rr[t]] = uint8_t(be[t]);
+                    w.split[soff + pp[t] * R1 + rr[t]] = uint16_t(be[t]);
                     if (convex && rr[t] == 0) w.rng[slot] = orng[t];
                 }
             }
@@ -1281,40 +1287,46 @@ __device__ void output_pass(const halda_batch &B, const halda_result &Rz, const 
 #define HALDA_SOLVE_WAVES_PER_SIMD 2  // occupancy target of the solve kernel (register budget)
 #endif
 
-__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_kernel(halda_batch B, halda_result Rz, const uint8_t *cls,
-                                                          int mmax, int r1max, int tab, int tab_kc,
-                                                          const int *hb_flag, int launch_id, int gated, int want) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// kGlobal = false: the slice lives in LDS (one wave per 64-thread workgroup). Instances whose shape
+// does not fit this launch's slice (M > mmax, R + 1 > r1max or M * RS > its table) are re-tagged
+// CLS_BIG for the global-table launch that follows (only launched when the batch's shape summary
+// exceeds the LDS budget). kGlobal = true: the same code on a per-wave slice of global scratch
+// (gtab + blockIdx.x * gstride bytes), sized from the full shape summary, no size limit but HBM.
+template <bool kGlobal>
+__device__ inline void solve_general(halda_batch B, halda_result Rz, uint8_t *cls, int mmax, int r1max, int tab,
+                                     int tab_kc, const int *hb_flag, int launch_id, int gated, int want,
+                                     unsigned char *slice_base) {
     const int lane = threadIdx.x;
     // gated: no k > 1 or wide instance in the batch; only k = 1 hand-backs (flagged) can be here
     if (gated && __hip_atomic_load(hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != launch_id) return;
     const Slice sl = make_slice(mmax, r1max, tab, tab_kc);
+    unsigned char *base = slice_base;
     WaveCtx w;
-    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
-    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
-    w.cost = reinterpret_cast<double *>(smem + sl.cost);
-    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
-    w.st0 = reinterpret_cast<int *>(smem + sl.st0);
-    w.st1 = reinterpret_cast<int *>(smem + sl.st1);
-    w.rng = reinterpret_cast<int2 *>(smem + sl.rng);
-    w.inc = reinterpret_cast<double *>(smem + sl.inc);
-    w.G = reinterpret_cast<double *>(smem + sl.G);
-    w.H = reinterpret_cast<double *>(smem + sl.H);
-    w.work = reinterpret_cast<double *>(smem + sl.work);
-    w.split = smem + sl.split;
+    w.rows = reinterpret_cast<int2 *>(base + sl.rows);
+    w.cyc = reinterpret_cast<double *>(base + sl.cyc);
+    w.cost = reinterpret_cast<double *>(base + sl.cost);
+    w.cnt = reinterpret_cast<int *>(base + sl.cnt);
+    w.st0 = reinterpret_cast<int *>(base + sl.st0);
+    w.st1 = reinterpret_cast<int *>(base + sl.st1);
+    w.rng = reinterpret_cast<int2 *>(base + sl.rng);
+    w.inc = reinterpret_cast<double *>(base + sl.inc);
+    w.G = reinterpret_cast<double *>(base + sl.G);
+    w.H = reinterpret_cast<double *>(base + sl.H);
+    w.work = reinterpret_cast<double *>(base + sl.work);
+    w.split = reinterpret_cast<uint16_t *>(base + sl.split);
 
     // this wave owns instances blockIdx.x + j * gridDim.x; a 64-wide window of
     // them is screened by one ballot over the verdict bytes
     const int S = gridDim.x;
-    for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
-        const int64_t mine = base + int64_t(lane) * S;
+    for (int64_t base_i = blockIdx.x; base_i < B.n_inst; base_i += int64_t(64) * S) {
+        const int64_t mine = base_i + int64_t(lane) * S;
         const bool open = mine < B.n_inst && cls[mine] == want;
         uint64_t todo = __ballot(open);
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
             Inst I;
-            I.inst = int(base + int64_t(bit) * S);
+            I.inst = int(base_i + int64_t(bit) * S);
             const int N = B.n_cols[I.inst];
             I.m = B.n_rows[I.inst];
             I.M = (N - 1) / 7;
@@ -1326,6 +1338,10 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
             I.Wd = B.row_ub[I.ro + I.m - 1];
             I.W = int(I.Wd);
             I.kc = B.c[I.co + I.iC];
+            if (!kGlobal && I.M > mmax) {  // wider than this slice: the global-table launch
+                if (lane == 0) cls[I.inst] = CLS_BIG;
+                continue;
+            }
             HALDA_STAMP(0);
 
             int bad = 0;
@@ -1333,6 +1349,10 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
             I.R1 = I.W - sumlo + 1;
             I.RS = odd_stride(I.R1);
             wave_sync();
+            if (!kGlobal && (I.R1 > r1max || int64_t(I.M) * I.RS > (I.kc > 0.0 ? tab_kc : tab))) {
+                if (lane == 0) cls[I.inst] = CLS_BIG;  // tables beyond this slice: the global-table launch
+                continue;
+            }
             HALDA_GSTAMP(1);
             bad |= row_pass(B, w, I, lane);
             wave_sync();
@@ -1356,6 +1376,22 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_ke
             HALDA_STAMP(6);
         }
     }
+}
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_kernel(
+    halda_batch B, halda_result Rz, uint8_t *cls, int mmax, int r1max, int tab, int tab_kc, const int *hb_flag,
+    int launch_id, int gated, int want) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    solve_general<false>(B, Rz, cls, mmax, r1max, tab, tab_kc, hb_flag, launch_id, gated, want, smem);
+}
+
+// Global-table variant: instances the LDS launches re-tagged CLS_BIG (and, in a batch whose summary
+// exceeds the LDS budget, nothing else).
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_solve_big_kernel(
+    halda_batch B, halda_result Rz, uint8_t *cls, int mmax, int r1max, int tab, int tab_kc, unsigned char *gtab,
+    int64_t gstride) {
+    solve_general<true>(B, Rz, cls, mmax, r1max, tab, tab_kc, nullptr, 0, 0, CLS_BIG,
+                        gtab + int64_t(blockIdx.x) * gstride);
 }
 
 // ---------------------------------------------------------------- k = 1 fast path
@@ -2434,6 +2470,11 @@ struct Ctx {
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
     size_t work_bytes = 0;
+    void *gtab = nullptr;  // per-wave global-memory slices of the big-table general launch
+    size_t gtab_bytes = 0;
+    hipEvent_t ev_order = nullptr;  // cross-stream ordering of consecutive launches on this context
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     void *fleet_scratch = nullptr;  // lowered batch + results of halda_solve_fleets
     size_t fleet_scratch_bytes = 0;
     halda_batch last_lowered = {};
@@ -2469,21 +2510,66 @@ int64_t slice_bytes_for(int mmax, int r1max, int tab, int tab_kc) {
     return make_slice(mmax, r1max, tab, tab_kc).total;
 }
 
+// On-chip budget of one general-kernel slice (LDS per CU is 160 KiB) and, for a batch whose shape
+// summary exceeds it, the capped LDS slice (2 waves per CU) plus the global-table launch's HBM budget.
+constexpr int64_t kLdsBudget = 160 * 1024;
+constexpr int64_t kLdsCapped = 80 * 1024;
+constexpr int64_t kGlobalTableBudget = int64_t(2) << 30;
+constexpr int kMaxR1 = 1 << 20;  // the screen rejects W >= 1e6 anyway
+
+struct GenShape {
+    int mmax, r1, tab, tab_kc;
+};
+
+// LDS shape of the general kernel's launches for a batch summary (full when it fits the budget).
+GenShape lds_shape(const GenShape &full, bool *big) {
+    const int64_t need = std::max(slice_bytes_for(full.mmax, full.r1, full.tab, 0),
+                                  slice_bytes_for(full.mmax, full.r1, 0, full.tab_kc));
+    *big = need > kLdsBudget;
+    if (!*big) return full;
+    GenShape g;
+    g.mmax = std::min(full.mmax, kK1MaxM);
+    g.r1 = std::min(full.r1, 128);
+    while (true) {
+        const int t = g.mmax * odd_stride(g.r1);
+        g.tab = full.tab > 0 ? std::min(full.tab, t) : 0;
+        g.tab_kc = full.tab_kc > 0 ? std::min(full.tab_kc, t) : 0;
+        const int64_t b = std::max(slice_bytes_for(g.mmax, g.r1, std::max(g.tab, 1), 0),
+                                   slice_bytes_for(g.mmax, g.r1, 0, g.tab_kc));
+        if (b <= kLdsCapped || g.r1 <= 8) break;
+        g.r1 = (g.r1 + 1) / 2;
+    }
+    g.tab = std::max(g.tab, 1);
+    return g;
+}
+
+// Device-side ordering across streams: the verdict bytes, the hand-back flag and the fleet scratch
+// are per context, so a launch on another stream than the previous one waits for everything
+// enqueued on that stream so far (same stream: stream order already serialises them).
+int order_after_previous(Ctx *ctx, hipStream_t s) {
+    if (ctx->have_last && ctx->last_stream != s) {
+        HIP_TRY(hipEventRecord(ctx->ev_order, ctx->last_stream));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->ev_order, 0));
+    }
+    ctx->last_stream = s;
+    ctx->have_last = true;
+    return HALDA_OK;
+}
+
 int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t stream) {
     if (in.n_inst <= 0) return HALDA_OK;
     if (in.max_cols < 1 || in.max_R1 < 1 || in.max_tab < 0 || in.max_tab_kc < 0)
         return fail(HALDA_E_ARG, "halda_batch shape summary (max_cols/max_R1/max_tab/max_tab_kc) not set");
-    if (in.max_R1 > 128) return fail(HALDA_E_ARG, "max_R1 > 128 (W - sum lb(w) must be < 128)");
+    if (in.max_R1 > kMaxR1) return fail(HALDA_E_ARG, "max_R1 > 2^20 (W - sum lb(w) must be < 2^20)");
     const int mmax = (in.max_cols - 1) / 7 + 1;
     // table sizes in doubles with the odd row stride used on chip
     // M * RS <= M * (R + 1) + M: the odd row stride costs at most one double per device
     const int64_t tab = std::max<int64_t>(1, in.max_tab > 0 ? int64_t(in.max_tab) + mmax : 0);
     const int64_t tab_kc = in.max_tab_kc > 0 ? int64_t(in.max_tab_kc) + mmax : 0;
-    if (tab > (1 << 24) || tab_kc > (1 << 24)) return fail(HALDA_E_ARG, "table summary out of range");
-    const int64_t lds = std::max(slice_bytes_for(mmax, in.max_R1, int(tab), 0),
-                                 slice_bytes_for(mmax, in.max_R1, 0, int(tab_kc)));
-    if (lds > 160 * 1024)
-        return fail(HALDA_E_ARG, "batch needs " + std::to_string(lds) + " B of LDS per solve wave (> 160 KiB)");
+    if (tab > (1 << 27) || tab_kc > (1 << 27)) return fail(HALDA_E_ARG, "table summary out of range (> 2^27)");
+    const GenShape full{mmax, in.max_R1, int(tab), int(tab_kc)};
+    bool big = false;
+    const GenShape ls = lds_shape(full, &big);
     const size_t n = size_t(in.n_inst);
     if (n > ctx->work_bytes) {
         if (ctx->work) HIP_TRY(hipFree(ctx->work));
@@ -2491,6 +2577,28 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         ctx->work_bytes = 0;
         HIP_TRY(hipMalloc(&ctx->work, (n + 255) & ~size_t(255)));
         ctx->work_bytes = (n + 255) & ~size_t(255);
+    }
+    // global tables of the big launch: one slice per resident wave, grown on demand
+    int64_t gstride = 0;
+    int ggrid = 0;
+    if (big) {
+        gstride = (make_slice(full.mmax, full.r1, full.tab, full.tab_kc).total + 255) & ~int64_t(255);
+        int per_cu = 0;
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_big_kernel), 0, &per_cu));
+        ggrid = int(std::max<int64_t>(
+            1, std::min<int64_t>({int64_t(ctx->cus) * per_cu, int64_t(n), kGlobalTableBudget / gstride})));
+        const size_t need = size_t(gstride) * size_t(ggrid);
+        if (need > ctx->gtab_bytes) {
+            if (ctx->gtab) HIP_TRY(hipFree(ctx->gtab));
+            ctx->gtab = nullptr;
+            ctx->gtab_bytes = 0;
+            HIP_TRY(hipMalloc(&ctx->gtab, need));
+            ctx->gtab_bytes = need;
+        }
+    }
+    {
+        const int rc = order_after_previous(ctx, stream);
+        if (rc != HALDA_OK) return rc;
     }
     uint8_t *cls = static_cast<uint8_t *>(ctx->work);
     const int launch_id = ++ctx->launch_id;  // tags this launch's k = 1 hand-backs (no reset needed)
@@ -2522,27 +2630,34 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     // general kernel, two launches with their own LDS slices: k > 1 instances (tables of the k > 1
     // shape only), then k = 1 instances of fleets wider than kK1MaxM devices and the fast path's
     // hand-backs (k = 1 tables). The first runs only when the shape summary admits k > 1 instances;
-    // the second is gated on the hand-back flag unless wide k = 1 fleets are possible.
+    // the second is gated on the hand-back flag unless wide k = 1 fleets are possible. A batch whose
+    // summary exceeds the LDS budget gets capped slices and a third launch on global-memory tables
+    // for the instances beyond them.
     const bool wide = (in.max_cols - 1) / 7 > kK1MaxM;
-    if (tab_kc > 0) {
-        const int64_t lds_kc = slice_bytes_for(mmax, in.max_R1, 0, int(tab_kc));
+    if (ls.tab_kc > 0) {
+        const int64_t lds_kc = slice_bytes_for(ls.mmax, ls.r1, 0, ls.tab_kc);
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_kc, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
-        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_kc), stream, in, out, cls, mmax,
-                           in.max_R1, 0, int(tab_kc), static_cast<const int *>(ctx->hb_flag), launch_id, 0,
-                           int(CLS_GEN));
+        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_kc), stream, in, out, cls, ls.mmax,
+                           ls.r1, 0, ls.tab_kc, static_cast<const int *>(ctx->hb_flag), launch_id, 0, int(CLS_GEN));
         HIP_TRY(hipGetLastError());
     }
     {
-        const int64_t lds_k1 = slice_bytes_for(mmax, in.max_R1, int(tab), 0);
+        const int64_t lds_k1 = slice_bytes_for(ls.mmax, ls.r1, ls.tab, 0);
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_k1, &per_cu));
         const int64_t cap = wide ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(cap, in.n_inst)));
-        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_k1), stream, in, out, cls, mmax,
-                           in.max_R1, int(tab), 0, static_cast<const int *>(ctx->hb_flag), launch_id, int(!wide),
+        hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_k1), stream, in, out, cls, ls.mmax,
+                           ls.r1, ls.tab, 0, static_cast<const int *>(ctx->hb_flag), launch_id, int(!wide),
                            int(CLS_GEN1));
+        HIP_TRY(hipGetLastError());
+    }
+    if (big) {
+        hipLaunchKernelGGL(halda_solve_big_kernel, dim3(unsigned(ggrid)), dim3(64), 0, stream, in, out, cls,
+                           full.mmax, full.r1, full.tab, full.tab_kc, static_cast<unsigned char *>(ctx->gtab),
+                           gstride);
         HIP_TRY(hipGetLastError());
     }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev1, stream));
@@ -2562,7 +2677,7 @@ int halda_last_error(char *buf, size_t len) {
 }
 
 int64_t halda_lds_bytes(int32_t max_cols, int32_t max_R1, int32_t max_tab, int32_t max_tab_kc) {
-    if (max_R1 < 1 || max_R1 > 128) return -1;
+    if (max_R1 < 1 || max_R1 > kMaxR1) return -1;
     const int mmax = (max_cols - 1) / 7 + 1;
     const int64_t tab = std::max<int64_t>(1, max_tab > 0 ? int64_t(max_tab) + mmax : 0);
     const int64_t tab_kc = max_tab_kc > 0 ? int64_t(max_tab_kc) + mmax : 0;
@@ -2594,7 +2709,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->xcd_swizzle = !(xs && xs[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess) {
+        hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) {
         halda_free(c);
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
@@ -2611,6 +2727,8 @@ void halda_free(void *ctx) {
     if (c->work) (void)hipFree(c->work);
     if (c->hb_flag) (void)hipFree(c->hb_flag);
     if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
+    if (c->gtab) (void)hipFree(c->gtab);
+    if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evs) (void)hipEventDestroy(c->evs);
@@ -2702,6 +2820,10 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     const int32_t *kh = ks;
     for (int j = 0; j < n_k; ++j)
         if (kh[j] < 1 || (j && kh[j] <= kh[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    {
+        const int rc = order_after_previous(c, s);  // fleet_scratch / last_lowered are per context
+        if (rc != HALDA_OK) return rc;
+    }
     const LowerDims D = lower_dims(F.max_devices, n_k);
     const int64_t n_inst = int64_t(F.n_fleets) * n_k;
     if (n_inst > (int64_t(1) << 30) || int64_t(F.n_fleets) * D.nnz > (int64_t(1) << 31) - 1)
@@ -2752,16 +2874,19 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     halda_batch b = {};
     b.n_inst = int32_t(n_inst);
     b.max_cols = int32_t(D.cols);
-    int r1_k1 = 0, r1_kc = 0;
+    int64_t r1_k1 = 0, r1_kc = 0;
     for (int j = 0; j < n_k; ++j) {
-        const int r1 = model->L / kh[j] - F.min_devices + 1;
+        const int64_t r1 = int64_t(model->L / kh[j]) - F.min_devices + 1;
         if (kh[j] == 1) r1_k1 = std::max(r1_k1, r1);
         else r1_kc = std::max(r1_kc, r1);
     }
-    b.max_R1 = std::max(1, std::max(r1_k1, r1_kc));
-    if (b.max_R1 > 128) return fail(HALDA_E_ARG, "L / k_min - min_devices + 1 > 128 (layers beyond one per device)");
-    b.max_tab = r1_k1 > 0 ? F.max_devices * r1_k1 : 0;
-    b.max_tab_kc = r1_kc > 0 ? F.max_devices * r1_kc : 0;
+    const int64_t r1max = std::max<int64_t>(1, std::max(r1_k1, r1_kc));
+    const int64_t tk1 = r1_k1 > 0 ? int64_t(F.max_devices) * r1_k1 : 0, tkc = r1_kc > 0 ? int64_t(F.max_devices) * r1_kc : 0;
+    if (r1max > kMaxR1 || tk1 > (1 << 27) || tkc > (1 << 27))
+        return fail(HALDA_E_ARG, "fleet shape out of range: (L / k_min - min_devices + 1) * max_devices > 2^27");
+    b.max_R1 = int32_t(r1max);
+    b.max_tab = int32_t(tk1);
+    b.max_tab_kc = int32_t(tkc);
     b.n_cols = O.n_cols;
     b.n_rows = O.n_rows;
     b.csr_off = O.csr_off;
@@ -2958,6 +3083,10 @@ int halda_solve_batch(void *ctx, const halda_batch *in_h, halda_result *out_h) {
     }
     char *base = static_cast<char *>(c->scratch);
     hipStream_t s = c->stream;
+    {
+        const int rc = order_after_previous(c, s);
+        if (rc != HALDA_OK) return rc;
+    }
     auto up = [&](size_t o, const void *src, size_t bytes) {
         return hipMemcpyAsync(base + o, src, bytes, hipMemcpyHostToDevice, s);
     };

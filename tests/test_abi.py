@@ -65,3 +65,17 @@ def test_product_path_has_no_oracle_import():
     for p in (REPO / "distilp_amd").rglob("*.py"):
         src = p.read_text()
         assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), p
+
+
+def test_lds_bytes_beyond_the_old_128_state_cap(lib):
+    """R + 1 > 128 is legal (the reference has no cap, halda_p_solver.py:72); shapes beyond the LDS
+    budget are reported as such (the library then runs the global-table launch)."""
+    assert 0 < lib.halda_lds_bytes(7 * 8 + 1, 249, 8 * 249, 8 * 121) < 160 * 1024
+    assert lib.halda_lds_bytes(7 * 100 + 1, 157, 100 * 157, 100 * 29) > 160 * 1024
+
+
+def test_integration_md_stub_is_the_committed_file():
+    """INTEGRATION.md path B shows integration/halda_milp.py verbatim (the GPU suite runs that file)."""
+    md = (REPO / "INTEGRATION.md").read_text()
+    code = (REPO / "integration" / "halda_milp.py").read_text()
+    assert "```python\n" + code + "```" in md
