@@ -1,27 +1,35 @@
 """Benchmark: HALDA MILP instances solved/s on MI355X (config C3 of BASELINE.json).
 
-Workload per GPU and step: 4096 seeded synthetic fleets of M = 64 devices
-(L = 80, model llama_3_70b/online, kv "4bit"), every fleet with all 9
-k-candidates of L = 80 -> 36,864 fixed-k MILP instances, solved exactly by ONE
-libhalda launch (halda_solve_batch_device) from inputs already resident in HBM.
-Weak scaling: rank r solves its own 4096 fleets (seeds r*4096 ...). No
-collective on the data path (fleets are independent); a barrier brackets the
-timed region and the max time over ranks is reported.
+Headline workload per GPU and step (weak scaling, the default): 4096 seeded synthetic
+fleets of M = 64 devices (L = 80, model llama_3_70b/online, kv "4bit"), each swept over
+all 9 k-candidates of L = 80 -> 36,864 fixed-k MILP instances, i.e. 4096 `halda_solve`
+k-sweeps: ONE libhalda `halda_solve_fleets` call per step takes the fleets' device-field
+table (resident in HBM) through the whole reference path -- lowering of every (fleet, k)
+(halda_p_solver.py:59-338), the exact solves (:340-353) and the argmin over k with the
+reference's tie rule (:391-414). Nothing is pre-lowered on the host.
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
-
-Extra JSON fields: roofline (dominant kernel halda_solve_kernel vs HBM peak,
-algorithmic bytes per launch defined in DESIGN.md §Measurement), cpu_baseline
-(the oracle = reference lowering + scipy/HiGHS, timed on ONE host core on a
-bounded sample of the same workload), feasible_instances_per_s, fleets_per_s,
-time_to_optimal_ms (median end-to-end halda_solve of one M=64 fleet).
+Beside it, in the same JSON line:
+  solve_only   the pre-lowered batch (host lowering, CSR in HBM) through the milp()
+               replacement alone (halda_solve_batch_device), with its own roofline;
+  strong       (N > 1) config C3 as a strong-scaling sweep: 4096 fleets in total, sharded
+               over the ranks (shard_bounds), max time over ranks;
+  cpu_baseline the oracle (reference lowering + scipy 1.15 / HiGHS 1.8.0, the reference's
+               arithmetic) on every host core this process may use, one pinned process per
+               core, on a bounded sample of the same fleets; also the 1-core rate;
+  time_to_optimal_ms  median wall time of one M = 64 halda_solve (Python call -> HALDAResult),
+               100 runs.
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, before any
+GPU call in this process) unless it already runs as one of them (WORLD_SIZE set, e.g. by the
+driver's own torch.distributed.run); --gpus must equal the world size it sees and the node
+must have N GPUs, else it exits with an error. Fleets are independent: no collective on the
+data path, a barrier brackets each timed region and the max time over ranks is reported.
 """
 
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import subprocess
@@ -37,56 +45,193 @@ sys.path.insert(0, str(REPO))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 KS_L80 = [1, 2, 4, 5, 8, 10, 16, 20, 40]
 METRIC = "HALDA MILP instances solved/sec (node), M=64 devs L=80; time-to-optimal"
+C3_FLEETS = 4096
+MALL_BYTES = 256 << 20  # Infinity Cache: rotate enough resident copies that every step reads HBM
+
+
+# ------------------------------------------------------------------ workload
+def fleet_seeds(args, rank: int, world: int, strong: bool):
+    if strong:
+        from distilp_amd.distributed import shard_bounds
+
+        lo, hi = shard_bounds(C3_FLEETS, rank, world)
+        return list(range(lo, hi))
+    return list(range(rank * args.fleets, (rank + 1) * args.fleets))
+
+
+def build_fleets(seeds, M: int):
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.synth import load_templates, synth_fleet
+
+    tpl = load_templates()
+    return [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)] for s in seeds]
+
+
+def load_model():
+    from distilp_amd.common import ModelProfileSplit
+    from distilp_amd.synth import load_model_dict
+
+    return ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
 
 
 def build_workload(rank: int, fleets: int, M: int, ks=None):
-    from distilp_amd.common import DeviceProfile, ModelProfileSplit
+    """(model, lowered fleets, CSR batch, refs) of rank `rank`'s weak-scaling fleets (diagnostic tools)."""
     from distilp_amd.solver.batch import assemble
     from distilp_amd.solver.lower import lower_fleet
-    from distilp_amd.synth import load_model_dict, load_templates, synth_fleet
 
-    model = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
-    tpl = load_templates()
-    lowered = []
-    for s in range(rank * fleets, (rank + 1) * fleets):
-        devs = [DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)]
-        lowered.append(lower_fleet(devs, model, "4bit"))
+    model = load_model()
+    lowered = [lower_fleet(devs, model, "4bit") for devs in build_fleets(range(rank * fleets, (rank + 1) * fleets), M)]
     batch, refs = assemble(lowered, [list(ks or KS_L80)] * len(lowered))
     return model, lowered, batch, refs
 
 
-def algorithmic_bytes(lowered, batch, refs):
-    """Bytes each launch must move: {kernel name: bytes per launch}.
+# ------------------------------------------------------------------ algorithmic bytes
+HDR = 4 + 4 + 8 + 8 + 8  # n_cols, n_rows, csr_off, col_off, row_off
+RES = 4 + 8 + 8 + 8 + 8  # status, obj_lin, dual_bound, gap, nodes
+DEV_FIELDS = 10 * 8 + 6 * 8 + 2  # FleetTable bytes per device (f64 x 10, int64 x 6, os_class, flags)
 
-    A solved (surviving) instance: its fleet's CSR once (row_ptr + col_idx/val, which contains the
-    equality row), its header (n_cols, n_rows, 3 offsets), c / col_lb / col_ub (8 B each) and
-    integrality (1 B) per column (which contain the w bounds and c[C]), row_lb / row_ub per row,
-    x out and the result scalars. A screened instance: its header, the equality row (two row_ptr
-    entries, M col_idx/val, its row bounds), lb of its M w-columns, c[C] and the verdict byte,
-    plus the result scalars when the screen settles it (M > W = L/k).
-      halda_screen_kernel + halda_solve_k1_kernel (default): every instance's screen bytes, then
-        the survivors' solve bytes;
-      halda_screen_k1_kernel (HALDA_TWO_PASS=0, one wave per instance): settled instances' screen
-        bytes + survivors' solve bytes + the verdict byte of every instance."""
-    hdr, res = 4 + 4 + 8 + 8 + 8, 4 + 8 + 8 + 8 + 8
-    solve, screen, fused = 0, 0, 0
-    fleets_solved = set()
+
+def algorithmic_bytes(lowered, refs, n_k: int):
+    """Bytes each launch must move, {kernel: bytes per launch}, for the lowered batch
+    `lowered` (host lowering of the same fleets, one FleetMILP per fleet) and its instances `refs`.
+
+    Solve (CSR) launches -- a solved (surviving) instance: its fleet's CSR once (row_ptr + col_idx/val,
+    which contains the equality row), its header, c / col_lb / col_ub (8 B each) and integrality
+    (1 B) per column, row_lb / row_ub per row, x out and the result scalars. A screened instance: its
+    header, the equality row (two row_ptr entries, M col_idx/val, its row bounds), lb of its M
+    w-columns, c[C] and the verdict byte, plus the result scalars when the screen settles it.
+    k-sweep launches (halda_solve_fleets) -- lowering: the fleet's device fields in; out the CSR, the
+    objective offsets and per instance its header plus, for W >= M, every column / row vector, for
+    W < M (the screen settles it) the w bounds, the C column and the equality-row bounds; pick: per
+    instance its status, per optimal instance its header, c and x, per fleet the offsets in and best k,
+    obj_value and w / n out, obj_by_k / status when requested (not in the bench)."""
+    solve = screen = fused = lower = pick = 0
+    fleets_seen, fleets_solved = set(), set()
     for ref in refs:
         fl = lowered[ref.fleet]
-        scr = hdr + 8 + 12 * fl.M + 16 + 8 * fl.M + 8 + 1
+        M, nc, nr = fl.M, fl.n_cols, fl.n_rows
+        csr = 4 * (nr + 1) + 12 * fl.nnz
+        scr = HDR + 8 + 12 * M + 16 + 8 * M + 8 + 1
         screen += scr
-        if ref.W - fl.M >= 0:
-            if ref.fleet not in fleets_solved:
+        if ref.fleet not in fleets_seen:
+            fleets_seen.add(ref.fleet)
+            lower += DEV_FIELDS * M + 8 + csr + 24
+            pick += 24 + 4 + 8 + 8 * M
+        lower += HDR
+        pick += 4
+        if ref.W - M >= 0:
+            if ref.fleet not in fleets_solved:  # a solved fleet's CSR is read once per launch
                 fleets_solved.add(ref.fleet)
-                solve += 4 * (fl.n_rows + 1) + 12 * fl.nnz
-                fused += 4 * (fl.n_rows + 1) + 12 * fl.nnz
-            one = hdr + 25 * fl.n_cols + 16 * fl.n_rows + 8 * fl.n_cols + res
+                solve += csr
+                fused += csr
+            one = HDR + 25 * nc + 16 * nr + 8 * nc + RES
             solve += one
             fused += one + 1
+            lower += 25 * nc + 16 * nr
+            pick += HDR + 16 * nc
         else:
-            screen += res
-            fused += scr + res
-    return {"halda_screen_k1_kernel": fused, "halda_screen_kernel": screen, "halda_solve_k1_kernel": solve}
+            screen += RES
+            fused += scr + RES
+            lower += 16 * M + 25 + 16
+    # fused k-sweep (no CSR): device fields in, per fleet best k / obj_value / w / n out
+    sweep = sum(DEV_FIELDS * fl.M + 8 + 4 + 8 + 8 * fl.M for fl in lowered)
+    return {"halda_screen_k1_kernel": fused, "halda_screen_kernel": screen, "halda_solve_k1_kernel": solve,
+            "halda_lower_kernel": lower, "halda_pick_kernel": pick, "halda_sweep_kernel": sweep}
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline_child(budget_s: float, M: int, core: int, first: int, count: int) -> None:
+    """One pinned process: the oracle (reference lowering + scipy HiGHS) on C3 fleets first ..
+    first+count-1 until the time budget is used; prints one JSON line."""
+    os.sched_setaffinity(0, {core})
+    from oracle import milp_oracle as mo
+
+    model = load_model()
+    fleets = build_fleets(range(first, first + count), M)
+    t0 = time.perf_counter()
+    n_inst = n_fleets = 0
+    while time.perf_counter() - t0 < budget_s and n_fleets < len(fleets):
+        mo.halda_solve_oracle(fleets[n_fleets], model, k_candidates=KS_L80, mip_gap=1e-4, kv_bits="4bit",
+                              solver="highs")
+        n_fleets += 1
+        n_inst += len(KS_L80)
+    print(json.dumps({"instances": n_inst, "fleets": n_fleets, "seconds": time.perf_counter() - t0}))
+
+
+def usable_cores():
+    """Cores this process may run on: its affinity set, capped by the cgroup CPU quota and by the CPU
+    share the GPU box states in OMP_NUM_THREADS (there nproc shows the whole machine)."""
+    cores = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None:
+        cores = cores[:quota]
+    share = os.environ.get("OMP_NUM_THREADS")  # the GPU box states the job's CPU share here (16)
+    if share and share.isdigit() and int(share) > 0:
+        cores = cores[:int(share)]
+    return cores, quota
+
+
+def run_cpu_baseline(budget_s: float, M: int):
+    """All usable cores (one pinned oracle process each, disjoint fleets), then one core alone."""
+    cores, quota = usable_cores()
+    per = 64  # fleets prepared per process (more than ~12 s of HiGHS work per core)
+
+    def spawn(core, first):
+        return subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-baseline-child",
+                                 "--cpu-budget", str(budget_s), "--M", str(M), "--cpu-core", str(core),
+                                 "--cpu-first", str(first), "--cpu-count", str(per)],
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+    def collect(procs):
+        recs = []
+        for p in procs:
+            out, err = p.communicate(timeout=budget_s * 6 + 300)
+            if p.returncode != 0:
+                raise RuntimeError(f"cpu baseline child failed: {err[-400:]}")
+            recs.append(json.loads(out.strip().splitlines()[-1]))
+        return recs
+
+    try:
+        allc = collect([spawn(c, i * per) for i, c in enumerate(cores)])
+        one = collect([spawn(cores[0], 0)])[0]
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "unit": "instances/s", "cores": len(cores), "kind": "port", "sample": f"failed: {e}"}
+    inst = sum(r["instances"] for r in allc)
+    secs = max(r["seconds"] for r in allc)
+    return {
+        "value": inst / secs, "unit": "instances/s", "cores": len(cores), "kind": "port",
+        "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
+        "one_core_value": one["instances"] / one["seconds"],
+        "sample": (f"{len(cores)} pinned processes (one per usable core), each the oracle on its own C3 fleets "
+                   f"for ~{budget_s:.0f} s: {sum(r['fleets'] for r in allc)} fleets x 9 k = {inst} instances in "
+                   f"{secs:.1f} s; one core alone: {one['instances']} instances in {one['seconds']:.1f} s. "
+                   "oracle/milp_oracle.py = the reference's lowering + scipy 1.15 HiGHS 1.8.0 (its arithmetic)"),
+    }
+
+
+# ------------------------------------------------------------------ GPU legs
+def timed(step, steps, torch, dev, dist, world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def to_device(batch, torch, dev):
@@ -105,73 +250,56 @@ def to_device(batch, torch, dev):
     return keep, out
 
 
-def cpu_baseline_child(budget_s: float, M: int) -> None:
-    """Runs in a child process pinned to one core: oracle (reference lowering + scipy HiGHS) on the
-    same C3 fleets (seeds 0, 1, ...) until the time budget is used; prints one JSON line."""
-    os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
-    from distilp_amd.common import DeviceProfile, ModelProfileSplit
-    from distilp_amd.synth import load_model_dict, load_templates, synth_fleet
-    from oracle import milp_oracle as mo
-
-    model = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
-    tpl = load_templates()
-    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M, tpl)] for s in range(512)]
-    t0 = time.perf_counter()
-    n_inst = n_fleets = 0
-    while time.perf_counter() - t0 < budget_s and n_fleets < len(fleets):
-        mo.halda_solve_oracle(fleets[n_fleets], model, k_candidates=KS_L80, mip_gap=1e-4, kv_bits="4bit",
-                              solver="highs")
-        n_fleets += 1
-        n_inst += len(KS_L80)
-    dt = time.perf_counter() - t0
-    print(json.dumps({"instances": n_inst, "fleets": n_fleets, "seconds": dt}))
-
-
-def run_cpu_baseline(budget_s: float, M: int):
-    try:
-        out = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--cpu-baseline-child",
-                              "--cpu-budget", str(budget_s), "--M", str(M)],
-                             capture_output=True, text=True, timeout=budget_s * 4 + 120, check=True)
-        rec = json.loads(out.stdout.strip().splitlines()[-1])
-    except Exception as e:  # noqa: BLE001
-        return {"value": None, "unit": "instances/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
-    return {
-        "value": rec["instances"] / rec["seconds"], "unit": "instances/s", "cores": 1, "kind": "port",
-        "sample": (f"{rec['fleets']} C3 fleets (seeds 0..{rec['fleets'] - 1}) x 9 k = {rec['instances']} instances "
-                   f"in {rec['seconds']:.1f} s; oracle/milp_oracle.py = reference lowering + scipy 1.15 HiGHS "
-                   f"1.8.0 (the reference's arithmetic), pinned to 1 core"),
-    }
-
-
-def time_to_optimal(model, M: int, runs: int = 30):
-    from distilp_amd.common import DeviceProfile
-    from distilp_amd.solver import halda_solve
-    from distilp_amd.synth import synth_fleet
-    import contextlib
-    import io
-
-    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(0, M)]
-    times = []
-    for i in range(runs + 3):
-        t0 = time.perf_counter()
-        with contextlib.redirect_stdout(io.StringIO()):
-            halda_solve(devs, model, mip_gap=1e-4, plot=False, kv_bits="4bit")
-        if i >= 3:
-            times.append((time.perf_counter() - t0) * 1e3)
-    return statistics.median(times)
+def roofline(phase_ms, alg_bytes, traffic_fn):
+    dom = max(phase_ms, key=phase_ms.get)
+    alg = alg_bytes.get(dom)
+    ms = phase_ms[dom]
+    achieved = alg / (ms * 1e-3) / 1e9 if alg else None
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic_fn(dom), "kernel": dom,
+            "kernel_ms": ms, "algorithmic_bytes_per_launch": alg, "launch_ms": phase_ms}
 
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py), or None when none covers this kernel."""
     cands = sorted((REPO / "profiles").glob("r*_pmc.json"))
-    if not cands:
-        return None
-    try:
-        rec = json.loads(cands[-1].read_text())
-        return rec["kernels"][kernel]["hbm_bytes_per_launch"]
-    except Exception:  # noqa: BLE001
-        return None
+    for c in reversed(cands):
+        try:
+            return json.loads(c.read_text())["kernels"][kernel]["hbm_bytes_per_launch"]
+        except Exception:  # noqa: BLE001
+            continue
+    return None
+
+
+def time_to_optimal(model, M: int, runs: int = 100):
+    import contextlib
+    import io
+
+    from distilp_amd.solver import halda_solve
+
+    devs = build_fleets([0], M)[0]
+    times = []
+    for i in range(runs + 5):
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            halda_solve(devs, model, mip_gap=1e-4, plot=False, kv_bits="4bit")
+        if i >= 5:
+            times.append((time.perf_counter() - t0) * 1e3)
+    return statistics.median(times)
+
+
+def launch_ranks(args) -> int:
+    """--gpus N from a plain `python bench.py`: start N ranks (one process per GPU) with
+    torch.distributed.run before this process touches the GPU, relay their output and exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -179,101 +307,148 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--fleets", type=int, default=4096, help="fleets per GPU per step")
+    ap.add_argument("--fleets", type=int, default=C3_FLEETS, help="fleets per GPU per step (weak scaling)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="headline: weak (fleets per GPU fixed) or strong (4096 fleets in total)")
     ap.add_argument("--M", type=int, default=64)
-    ap.add_argument("--copies", type=int, default=2, help="resident copies of the batch, used in turn")
+    ap.add_argument("--copies", type=int, default=0, help="resident copies per leg (0: enough to exceed the MALL)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-tto", action="store_true")
     ap.add_argument("--ks", type=str, default="", help="diagnostic: comma-separated k-candidates instead of C3's")
     ap.add_argument("--cpu-baseline-child", action="store_true")
+    ap.add_argument("--cpu-core", type=int, default=0)
+    ap.add_argument("--cpu-first", type=int, default=0)
+    ap.add_argument("--cpu-count", type=int, default=64)
     args = ap.parse_args()
     if args.cpu_baseline_child:
-        cpu_baseline_child(args.cpu_budget, args.M)
-        return
+        cpu_baseline_child(args.cpu_budget, args.M, args.cpu_core, args.cpu_first, args.cpu_count)
+        return 0
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch_ranks(args)
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        return 2
+
     cpu_base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_base = run_cpu_baseline(args.cpu_budget, args.M)  # before any GPU work, in a child process
+        cpu_base = run_cpu_baseline(args.cpu_budget, args.M)  # before any GPU work, in child processes
 
     import torch
     import torch.distributed as dist
 
+    n_dev = torch.cuda.device_count()
+    if n_dev < world or local >= n_dev:
+        print(f"bench.py: --gpus {args.gpus} needs {world} GPUs on this node, {n_dev} visible", file=sys.stderr)
+        return 2
+    rccl_world = 1
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
+        rccl_world = dist.get_world_size()
+        if rccl_world != args.gpus:
+            print(f"bench.py: RCCL world size {rccl_world} != --gpus {args.gpus}", file=sys.stderr)
+            return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     from distilp_amd.solver._libhalda import get_context
+    from distilp_amd.solver.batch import assemble
+    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table
+    from distilp_amd.solver.lower import lower_fleet
 
     t_setup = time.perf_counter()
-    ks = [int(k) for k in args.ks.split(",")] if args.ks else None
-    model, lowered, batch, refs = build_workload(rank, args.fleets, args.M, ks)
-    # args.copies resident copies of the batch, used in turn: the bytes one step reads (~221 MB at C3)
-    # times the copies exceed the 256 MiB Infinity Cache, so every step reads its inputs from HBM
-    copies = [to_device(batch, torch, dev) for _ in range(args.copies)]
-    keep, out = copies[0]
+    ks = [int(k) for k in args.ks.split(",")] if args.ks else KS_L80
+    model = load_model()
+    strong_head = args.scaling == "strong"
+    seeds = fleet_seeds(args, rank, world, strong_head)
+    fleets = build_fleets(seeds, args.M)
+    table = fleet_table(fleets, model)
     ctx = get_context(local)
-    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the kernels and the events share it
-    cptrs = [({f: t.data_ptr() for f, t in k.items()}, {f: t.data_ptr() for f, t in o.items()}) for k, o in copies]
+    stream = torch.cuda.Stream(dev)
+    sref = stream.cuda_stream
+
+    # ---- headline: the k-sweep from resident device-field tables (rotating copies > the MALL)
+    tbytes = DeviceFleetTable(table, model, ks, 0.5, dev).nbytes()
+    n_sw = args.copies or max(2, min(32, math.ceil(2 * MALL_BYTES / max(tbytes, 1))))
+    sweeps = [DeviceFleetTable(table, model, ks, 0.5, dev) for _ in range(n_sw)]
     turn = [0]
+
+    def sweep_step():
+        sweeps[turn[0] % n_sw].launch(ctx, sref)
+        turn[0] += 1
+
+    # ---- solve-only leg: the same fleets lowered on the host, CSR batch resident in HBM
+    lowered = [lower_fleet(devs, model, "4bit") for devs in fleets]
+    batch, refs = assemble(lowered, [ks] * len(lowered))
+    n_so = args.copies or 2
+    copies = [to_device(batch, torch, dev) for _ in range(n_so)]
+    cptrs = [({f: t.data_ptr() for f, t in k.items()}, {f: t.data_ptr() for f, t in o.items()}) for k, o in copies]
+
+    def solve_step():
+        ptrs, optrs = cptrs[turn[0] % n_so]
+        turn[0] += 1
+        ctx.solve_device(ptrs, batch, optrs, stream=sref)
+
     setup_s = time.perf_counter() - t_setup
 
-    def step():
-        ptrs, optrs = cptrs[turn[0] % len(cptrs)]
-        turn[0] += 1
-        ctx.solve_device(ptrs, batch, optrs, stream=stream.cuda_stream)
-
+    # warm-up and sanity: the sweep's per-fleet answers equal the solve-only leg's k = 1 solves
     for _ in range(args.warmup):
-        step()
+        sweep_step()
+        solve_step()
     torch.cuda.synchronize(dev)
-    # sanity: statuses of this workload (k = 1 feasible, k > 1 infeasible when M > W)
-    st = out["status"].cpu().numpy()
+    st = copies[0][1]["status"].cpu().numpy()
     n_opt, n_inf = int((st == 0).sum()), int((st == 2).sum())
     if n_opt + n_inf != batch.n_inst:
         raise RuntimeError(f"unexpected statuses: {np.unique(st, return_counts=True)}")
+    bk = sweeps[0].out["best_k"].cpu().numpy()
+    if not (bk > 0).all():
+        raise RuntimeError("a fleet without a feasible k in the sweep")
 
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ctx.set_timing(False)  # no per-launch instrumentation events inside the timed region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    seq_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the kernels' stream: whole launch sequence
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # per-launch device times (HIP events recorded by libhalda on the kernels' stream around each
-    # launch), after the timed region; the dominant kernel is the longest of them
+    ctx.set_timing(False)  # no per-launch instrumentation events inside the timed regions
+    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world)
+    el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
+    el_strong = None
+    if world > 1 and not strong_head:
+        s_seeds = fleet_seeds(args, rank, world, True)
+        s_table = fleet_table(build_fleets(s_seeds, args.M), model)
+        n_st = max(2, min(32, math.ceil(2 * MALL_BYTES / max(DeviceFleetTable(s_table, model, ks, 0.5, dev).nbytes(), 1))))
+        s_sweeps = [DeviceFleetTable(s_table, model, ks, 0.5, dev) for _ in range(n_st)]
+        sturn = [0]
+
+        def strong_step():
+            s_sweeps[sturn[0] % n_st].launch(ctx, sref)
+            sturn[0] += 1
+
+        for _ in range(args.warmup):
+            strong_step()
+        el_strong = timed(strong_step, args.steps, torch, dev, dist, world)
+
+    # per-launch device times (HIP events recorded by libhalda on the kernels' stream), after the
+    # timed regions; the dominant launch of each leg is the longest
     ctx.set_timing(True)
-    phases = []
+    fl_ms, so_ms = [], []
     for _ in range(max(3, min(args.steps, 10))):
-        step()
+        sweep_step()
         torch.cuda.synchronize(dev)
-        phases.append(ctx.last_phase_ms())
-    phase_ms = {k: statistics.mean(p[k] for p in phases) for k in phases[0]}
-    dom = max(phase_ms, key=phase_ms.get)
+        fl_ms.append(ctx.last_fleet_ms())
+        solve_step()
+        torch.cuda.synchronize(dev)
+        so_ms.append(ctx.last_phase_ms())
+    fl_mean = {k: statistics.mean(p.get(k, 0.0) for p in fl_ms) for k in fl_ms[0]}
+    so_mean = {k: statistics.mean(p[k] for p in so_ms) for k in so_ms[0]}
+    alg = algorithmic_bytes(lowered, refs, len(ks))
 
-    total_inst = batch.n_inst * world * args.steps
-    value = total_inst / elapsed
-    alg_bytes = algorithmic_bytes(lowered, batch, refs)
-    alg = alg_bytes.get(dom, batch.n_inst)  # the general kernel alone only scans the verdict bytes
-    solve_ms = phase_ms[dom]
-    achieved = alg / (solve_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(dom)
+    inst_rank = len(fleets) * len(ks)
+    total = inst_rank * world * args.steps if not strong_head else C3_FLEETS * len(ks) * args.steps
+    value = total / el_sweep
+    n_fleets_total = (len(fleets) * world if not strong_head else C3_FLEETS) * args.steps
     if rank == 0:
-        tto = time_to_optimal(model, args.M) if world == 1 else None
+        tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -281,36 +456,39 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": el_sweep / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded C3 fleets, distilp_amd/synth.py)",
             "config": {
-                "workload": f"C3: {args.fleets} synthetic M={args.M} fleets x 9 k-candidates per GPU "
-                            "(L=80, llama_3_70b/online, kv 4bit), one exact libhalda launch per step",
-                "instances_per_step_per_gpu": batch.n_inst,
+                "workload": (f"C3: {len(fleets) if not strong_head else C3_FLEETS} synthetic M={args.M} fleets x "
+                             f"{len(ks)} k-candidates per {'GPU' if not strong_head else 'node'} (L=80, "
+                             "llama_3_70b/online, kv 4bit): one halda_solve_fleets k-sweep per step from the "
+                             "fleets' device-field tables resident in HBM (GPU lowering + exact solves + argmin "
+                             "over k)"),
+                "instances_per_step_per_gpu": inst_rank,
                 "feasible_per_step_per_gpu": n_opt,
                 "parallelism": f"dp{world} (fleets sharded, no collective on the data path)",
-                "resident_copies": args.copies,
+                "rccl_world_size": rccl_world,
+                "resident_copies": n_sw,
             },
-            "feasible_instances_per_s": n_opt * world * args.steps / elapsed,
-            "fleets_per_s": args.fleets * world * args.steps / elapsed,
+            "feasible_instances_per_s": value * n_opt / batch.n_inst,
+            "fleets_per_s": n_fleets_total / el_sweep,
             "time_to_optimal_ms": tto,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": dom,
-                "kernel_ms": solve_ms,
-                "algorithmic_bytes_per_launch": alg,
-                "sequence_ms": seq_ms,
-                "launch_ms": phase_ms,
-                "algorithmic_bytes": alg_bytes,
+            "roofline": roofline(fl_mean, alg, pmc_traffic),
+            "solve_only": {
+                "what": "same fleets lowered on the host beforehand; halda_solve_batch_device on the CSR batch "
+                        "resident in HBM (the milp() replacement alone)",
+                "instances_per_s": inst_rank * world * args.steps / el_solve,
+                "ms_per_step": el_solve / args.steps * 1e3,
+                "resident_copies": n_so,
+                "roofline": roofline(so_mean, alg, pmc_traffic),
+            },
+            "strong": None if el_strong is None else {
+                "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,
+                "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
             },
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,
@@ -318,7 +496,8 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

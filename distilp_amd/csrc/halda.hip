@@ -1031,18 +1031,28 @@ __device__ inline void table_entry(const Dev &d, const WaveCtx &w, const Inst &I
     if (I.kc > 0.0) w.H[i * I.RS + e] = h;
 }
 
+// Device records of an instance decoded from its CSR (load_dev).
+struct CsrSrc {
+    const halda_batch *B;
+    int64_t co;
+    int M;
+    double Wd;
+    __device__ inline void load(Dev &d, const WaveCtx &w, int i) const { load_dev(d, *B, w, co, M, i, Wd); }
+};
+
 // Table pass (lane = device): G[i][e] (and H[i][e] for k > 1), w = lb + e, one
 // incremental chain per device (split_step reuses the previous argmin).
 // Fleets of at most 32 devices spread each device's chain over P = 64 / M lanes
 // (each starts its stretch of e with a full split search): the least minimiser
 // n*(w) is the same either way, so G and H are too.
-__device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I, int lane) {
+template <class Src>
+__device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int lane) {
     if (I.M <= 32) {
         const int P = 64 / I.M, chunk = (I.R1 + P - 1) / P;
         const int i = lane / P, p = lane - i * P;
         if (i < I.M) {
             Dev d;
-            load_dev(d, B, w, I.co, I.M, i, I.Wd);
+            src.load(d, w, i);
             int n = 0;
             bool have = false;
             const int e1 = min(I.R1, (p + 1) * chunk);
@@ -1052,7 +1062,7 @@ __device__ void table_pass(const halda_batch &B, const WaveCtx &w, const Inst &I
     }
     for (int i = lane; i < I.M; i += 64) {
         Dev d;
-        load_dev(d, B, w, I.co, I.M, i, I.Wd);
+        src.load(d, w, i);
         int n = 0;
         bool have = false;
         for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
@@ -1363,7 +1373,7 @@ __device__ inline void solve_general(halda_batch B, halda_result Rz, uint8_t *cl
                 continue;
             }
             HALDA_GSTAMP(3);
-            table_pass(B, w, I, lane);
+            table_pass(CsrSrc{&B, I.co, I.M, I.Wd}, w, I, lane);
             wave_sync();
             HALDA_GSTAMP(4);
             int64_t nodes = 0;
@@ -2102,6 +2112,95 @@ __device__ inline double f_over_s(bool present, double f, double s) {
     return present ? (s > 0.0 ? 0.0 + f / s : 0.0) : 0.0;
 }
 
+// Per-device coefficients of the fixed-k MILP (dense_common.py:25-126 and the penalties of
+// halda_p_solver.py:195-224) in the reference's operation order; shared by the lowering kernel
+// (CSR out) and the sweep kernel (records straight into registers), so both see the same bits.
+struct DevCoef {
+    double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+};
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    DevCoef o;
+    const double bp = Mo.b_prime;
+    const uint8_t fl = F.flags[g];
+    const int cls = F.os_class[g];
+    const double Tc = F.T_cpu[g], tkc = F.t_kvcpy_cpu[g], tkg = F.t_kvcpy_gpu[g];
+    const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu_b1[g]);
+    const bool hb = fl & HALDA_DEV_GPU;
+    const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu_b1[g]) : 0.0;
+    const double tg = hb ? F.T_gpu[g] : 1.0;
+    o.alpha = (cpu + tkc) + (bp / Tc);
+    const double beta = hb ? ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc) : 0.0;
+    o.b = cls == 1 ? 0.0 : beta;
+    o.xi = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
+    const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+    o.bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.c_cpu[g]);
+    const double sd = fmax(1.0, F.s_disk[g]);
+    o.p_bp = bp / sd;
+    o.p_b = Mo.b_layer / sd;
+    o.p_v = cls == 2 ? o.p_b : o.p_bp;
+    o.cst = o.xi + F.t_comm[g];
+    return o;
+}
+
+// Right-hand sides of the capacity rows (halda_p_solver.py:227-277).
+__device__ inline double rhs_ram(const halda_fleets &F, int64_t g, int set, double bcio) {
+    if (set == 1) return double(F.d_avail_ram[g]) - bcio;
+    if (set == 2) return double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
+    return double(F.d_avail_ram[g] + F.swap[g]) - bcio;
+}
+__device__ inline double rhs_cuda(const halda_fleets &F, int64_t g) {
+    return double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
+}
+__device__ inline double rhs_metal(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    const double head = (F.flags[g] & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+    return double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
+}
+
+// Objective constants of one fleet (lane-parallel loads, the reference's sequential sums over
+// readlane): sum t_comm and sum xi in device order, kappa (dense_common.py:211-230) with its
+// M1 part before its M3 part (:226). Uniform on every lane.
+__device__ inline void fleet_offsets(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
+                                     double &tsum, double &xsum, double &kappa) {
+    tsum = 0.0;
+    xsum = 0.0;
+    double tail1 = 0.0;
+    int hi = -1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const double tc = F.t_comm[g];
+        const double xv = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const uint64_t heads = __ballot(i0 + lane < M && (F.flags[g] & HALDA_DEV_HEAD));
+        if (hi < 0 && heads) hi = i0 + __builtin_ctzll(heads);
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q) {
+            tsum += bcast(tc, q);
+            xsum += bcast(xv, q);
+            const int cq = bcast(cls, q);
+            if (cq == 1) tail1 += bcast(tl, q);
+        }
+    }
+    double tail = tail1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q)
+            if (bcast(cls, q) == 3) tail += bcast(tl, q);
+    }
+    const int64_t h = d0 + (hi < 0 ? 0 : hi);
+    double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
+    total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
+    total += Mo.b_in / (Mo.V * F.s_disk[h]);
+    total += Mo.b_out / F.s_disk[h];
+    kappa = total + tail;
+}
+
 struct LowerOut {
     halda_batch b;         // arrays written (device pointers, const-cast by the kernel)
     int32_t *n_cols, *n_rows, *row_ptr, *col_idx;
@@ -2170,37 +2269,12 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         }
     };
     // ---- per-device coefficients (lower._device_arrays order); lane i's own device is computed once
-    auto coeff_calc = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
-                          double &bcio, double &xi) {
-        const int64_t g = d0 + i;
-        const uint8_t fl = F.flags[g];
-        const int cls = F.os_class[g];
-        const double Tc = F.T_cpu[g], tkc = F.t_kvcpy_cpu[g], tkg = F.t_kvcpy_gpu[g];
-        const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu_b1[g]);
-        const bool hb = fl & HALDA_DEV_GPU;
-        const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu_b1[g]) : 0.0;
-        const double tg = hb ? F.T_gpu[g] : 1.0;
-        alpha = (cpu + tkc) + (bp / Tc);
-        const double beta = hb ? ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc) : 0.0;
-        b = cls == 1 ? 0.0 : beta;
-        xi = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
-        const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-        bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.c_cpu[g]);
-        const double sd = fmax(1.0, F.s_disk[g]);
-        p_bp = bp / sd;
-        p_b = Mo.b_layer / sd;
-        p_v = cls == 2 ? p_b : p_bp;
-        cst = xi + F.t_comm[g];
-    };
-    double m_alpha = 0, m_b = 0, m_pbp = 0, m_pb = 0, m_pv = 0, m_cst = 0, m_bcio = 0, m_xi = 0;
-    if (lane < M) coeff_calc(lane, m_alpha, m_b, m_pbp, m_pb, m_pv, m_cst, m_bcio, m_xi);
+    DevCoef mine = {};
+    if (lane < M) mine = dev_coef(Mo, F, d0 + lane);
     auto coeff = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
                      double &bcio, double &xi) {
-        if (i == lane) {
-            alpha = m_alpha; b = m_b; p_bp = m_pbp; p_b = m_pb; p_v = m_pv; cst = m_cst; bcio = m_bcio; xi = m_xi;
-        } else {
-            coeff_calc(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
-        }
+        const DevCoef c = i == lane ? mine : dev_coef(Mo, F, d0 + i);
+        alpha = c.alpha; b = c.b; p_bp = c.p_bp; p_b = c.p_b; p_v = c.p_v; cst = c.cst; bcio = c.bcio; xi = c.xi;
     };
     // 1. link rows n_i - w_i <= 0
     emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
@@ -2222,9 +2296,7 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
             put(wr, e0, c0, i, bp);
             if (set == 3) put(wr, e0, c0, M + i, -bp);
             put(wr, e0, c0, (1 + set) * M + i, -bp);
-            if (set == 1) r0 = double(F.d_avail_ram[g]) - bcio;
-            else if (set == 2) r0 = double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
-            else r0 = double(F.d_avail_ram[g] + F.swap[g]) - bcio;
+            r0 = rhs_ram(F, g, set, bcio);
             return 1;
         });
     }
@@ -2233,9 +2305,8 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         const int64_t g = d0 + i;
         const uint8_t fl = F.flags[g];
         const bool cu = fl & HALDA_DEV_CUDA_OK, me = fl & HALDA_DEV_METAL_OK;
-        const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-        const double rc = double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
-        const double rm = double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
+        const double rc = rhs_cuda(F, g);
+        const double rm = rhs_metal(Mo, F, g);
         if (cu) {
             put(wr, e0, c0, M + i, bp);
             put(wr, e0, c0, 5 * M + i, -bp);
@@ -2335,49 +2406,361 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
         O.col_off[inst] = co;
         O.row_off[inst] = ro;
     }
-    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230).
-    // Lane-parallel loads, then the reference's sequential sums over readlane (no serial memory chain).
-    double tsum = 0.0, xsum = 0.0, tail1 = 0.0, tail3 = 0.0;
-    int hi = -1;
-    for (int i0 = 0; i0 < M; i0 += 64) {
-        const int i = min(i0 + lane, M - 1);
-        const int64_t g = d0 + i;
-        const double tc = F.t_comm[g];
-        const double xv = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
-        const int cls = F.os_class[g];
-        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
-        const uint64_t heads = __ballot(i0 + lane < M && (F.flags[g] & HALDA_DEV_HEAD));
-        if (hi < 0 && heads) hi = i0 + __builtin_ctzll(heads);
-        const int n = min(64, M - i0);
-        for (int q = 0; q < n; ++q) {
-            tsum += bcast(tc, q);
-            xsum += bcast(xv, q);
-            const int cq = bcast(cls, q);
-            if (cq == 1) tail1 += bcast(tl, q);
-        }
-        (void)tail3;
-    }
-    // the M3 part of the tail follows all of M1 (dense_common.py:226: M1 + M3 order)
-    double tail = tail1;
-    for (int i0 = 0; i0 < M; i0 += 64) {
-        const int i = min(i0 + lane, M - 1);
-        const int64_t g = d0 + i;
-        const int cls = F.os_class[g];
-        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
-        const int n = min(64, M - i0);
-        for (int q = 0; q < n; ++q)
-            if (bcast(cls, q) == 3) tail += bcast(tl, q);
-    }
+    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230)
+    double tsum, xsum, kappa;
+    fleet_offsets(Mo, F, d0, M, lane, tsum, xsum, kappa);
     if (lane == 0) {
-        const int64_t h = d0 + (hi < 0 ? 0 : hi);
-        double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
-        total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
-        total += Mo.b_in / (Mo.V * F.s_disk[h]);
-        total += Mo.b_out / F.s_disk[h];
         O.offs[3 * f + 0] = tsum;
         O.offs[3 * f + 1] = xsum;
-        O.offs[3 * f + 2] = total + tail;
+        O.offs[3 * f + 2] = kappa;
     }
+}
+
+// ---------------------------------------------------------------- fused k-sweep
+// halda_sweep_kernel: the whole `halda_solve` k-sweep of a fleet (halda_p_solver.py:369-436) in
+// one wave, from the fleet's device-field table, without materialising the MILPs. For every
+// k-candidate the wave builds, per device, exactly the record that decoding the lowered CSR
+// yields (load_dev of decode_cap_row / decode_cycle_row output, with the same rejections),
+// straight from the coefficients the lowering kernel writes into the CSR (dev_coef / rhs_* are
+// shared, so the values are the same bits); then settles bound-infeasible k (L / k < M), solves
+// k = 1 by the register greedy of the k = 1 fast path and the rest (k > 1, fleets wider than
+// 64 devices, fast-path fallbacks) by the general kernel's tables + DP / threshold scan, and keeps
+// the best k by the reference's rule (ascending k, strict "<" on obj_value, :407) in registers.
+// obj_value = c.x + sum t_comm + sum xi + kappa is formed in a fixed order (per-device costs
+// summed by a wave reduction, + (k - 1) C, + the fleet constants).
+//
+// kTables = false: no LDS; a fleet that needs a table is flagged (fflag[f] = 1, hb_flag = launch)
+// and left to the next launch. kTables = true: tables in the LDS slice (kGlobal = false) or in a
+// per-wave global slice (kGlobal = true); want = 1 selects the flagged fleets only (gated on the
+// hand-back flag), want = 0 every fleet.
+
+// Device record of table entry g for W layers (lb(w) = 1, bounds scaled by W as the lowering
+// writes them); bad = 1 when the lowered rows would be rejected by decode (UNSUPPORTED).
+struct FieldDev {
+    Dev d;
+    int cls, gpu, bad;
+};
+
+__device__ inline FieldDev field_dev(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    FieldDev o;
+    const DevCoef c = dev_coef(Mo, F, g);
+    const double bp = Mo.b_prime;
+    const uint8_t fl = F.flags[g];
+    o.cls = F.os_class[g];
+    o.gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1 : 0;
+    Dev &d = o.d;
+    d.cw = c.alpha; d.cn = c.b; d.cs0 = c.p_bp; d.cs1 = c.p_b; d.cs2 = c.p_bp; d.cs3 = c.p_v;
+    // cycle rows: busy + z - C <= -cst, busy + F - z - C <= -cst (w entries alpha, alpha + b'/s_disk)
+    d.r1w = c.alpha;
+    d.r2w = c.alpha + c.p_bp;
+    d.rhs1 = -c.cst;
+    d.rhs2 = -c.cst;
+    d.wlo = 1; d.whi = 0; d.nlo = 0; d.nhi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        d.slo[j] = 0; d.shi[j] = 0; d.us[j] = 0; d.vs[j] = 0; d.Ks[j] = kNoRow;
+    }
+    // the link row n - w <= 0 (scale 1: K = floor(0 + 1e-9) = 0)
+    d.uf[0] = -1; d.vf[0] = 1; d.Kf[0] = 0;
+    d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
+    int bad = !(fabs(c.cst) < 1e300);  // cycle-row rhs
+    bad |= !(c.p_bp >= 0.0) || !(c.p_b >= 0.0) || !(c.p_v >= 0.0);  // device_pass: slack prices >= 0
+    // capacity rows b' u w + b' v n - b' s <= rhs -> s >= u w + v n + ceil(-rhs / b' - eps)
+    auto cap = [&](int kind, int u, int v, double rhs) {
+        if (!(bp > 0.0) || !(fabs(rhs) < 1e300)) {
+            bad = 1;
+            return;
+        }
+        const double kk = ceil(-rhs / bp - kSlackEps);
+        if (!(fabs(kk) < 1e8)) {
+            bad = 1;
+            return;
+        }
+        d.us[kind] = u;
+        d.vs[kind] = v;
+        d.Ks[kind] = max(d.Ks[kind], int(kk));
+    };
+    if (o.cls == 1) cap(0, 1, 0, rhs_ram(F, g, 1, c.bcio));
+    else if (o.cls == 2) {
+        if (fl & HALDA_DEV_METAL_AVAIL) cap(1, 1, 0, rhs_ram(F, g, 2, c.bcio));
+    } else cap(2, 1, -1, rhs_ram(F, g, 3, c.bcio));
+    if (fl & HALDA_DEV_CUDA_OK) cap(3, 0, 1, rhs_cuda(F, g));
+    if (fl & HALDA_DEV_METAL_OK) cap(3, 0, 1, rhs_metal(Mo, F, g));
+    o.bad = bad;
+    return o;
+}
+
+__device__ inline void field_bounds(FieldDev &f, int W) {
+    f.d.whi = W;
+    f.d.nhi = f.gpu ? W : 0;
+    f.d.shi[0] = f.cls == 1 ? W : 0;
+    f.d.shi[1] = f.cls == 2 ? W : 0;
+    f.d.shi[2] = f.cls == 3 ? W : 0;
+    f.d.shi[3] = f.gpu ? W : 0;
+}
+
+// Device records of a fleet straight from its table (the sweep's table path).
+struct FieldSrc {
+    const halda_model *Mo;
+    const halda_fleets *F;
+    int64_t d0;
+    int W;
+    __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
+        FieldDev f = field_dev(*Mo, *F, d0 + i);
+        field_bounds(f, W);
+        d = f.d;
+    }
+};
+
+struct SweepArgs {
+    halda_model Mo;
+    halda_fleets F;
+    const int32_t *ks;
+    int n_k;
+    halda_fleet_result out;
+    int64_t xstride;
+    uint8_t *fflag;  // per fleet: 1 = needs the table launch
+    int *hb_flag;
+    int launch_id;
+    int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
+    unsigned char *gtab;           // kGlobal: per-wave slices
+    int64_t gstride;
+    int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
+};
+
+// x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
+// by the lane of each device when the caller asked for them.
+__device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
+                              const Dev &d) {
+    if (A.out.x) {
+        double *x = A.out.x + inst * A.xstride;
+        x[i] = double(wl); x[M + i] = double(n);
+        x[2 * M + i] = double(s[0]); x[3 * M + i] = double(s[1]); x[4 * M + i] = double(s[2]);
+        x[5 * M + i] = double(s[3]); x[6 * M + i] = z;
+    }
+    if (A.out.c) {
+        double *c = A.out.c + inst * A.xstride;
+        c[i] = d.cw; c[M + i] = d.cn; c[2 * M + i] = d.cs0; c[3 * M + i] = d.cs1; c[4 * M + i] = d.cs2;
+        c[5 * M + i] = d.cs3; c[6 * M + i] = 0.0;
+    }
+}
+
+template <bool kTables, bool kGlobal>
+__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lane) {
+    const halda_model &Mo = A.Mo;
+    const halda_fleets &F = A.F;
+    const int64_t d0 = F.dev_off[f];
+    const int M = int(F.dev_off[f + 1] - d0);
+    const bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
+    FieldDev me = {};
+    int bad = 0;
+    if (regs && lane < M) me = field_dev(Mo, F, d0 + lane);
+    if (regs) bad = lane < M ? me.bad : 0;
+    else
+        for (int i = lane; i < M; i += 64) bad |= field_dev(Mo, F, d0 + i).bad;
+    bad = wave_or(bad);
+    double tsum = 0.0, xsum = 0.0, kappa = 0.0;
+    if (M > 0) fleet_offsets(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    double best = kInf;
+    int best_k = 0;
+    for (int j = 0; j < A.n_k; ++j) {
+        const int k = A.ks[j];
+        const int W = Mo.L / k;
+        const int64_t inst = int64_t(f) * A.n_k + j;
+        const double kc = double(k - 1);
+        int st;
+        double obj = kInf;
+        bool improved = false;
+        if (!(W < 1000000)) st = HALDA_STATUS_UNSUPPORTED;  // the screen's W < 1e6
+        else if (M > W) st = HALDA_STATUS_INFEASIBLE;      // sum lb(w) = M > W (HiGHS presolve)
+        else if (M == 0) st = W > 0 ? HALDA_STATUS_INFEASIBLE : HALDA_STATUS_OPTIMAL;  // x = [C = 0]
+        else if (bad) st = HALDA_STATUS_UNSUPPORTED;
+        else {
+            int rc = K1_FALLBACK, e = 0, rounds = 0;
+            if (k == 1 && regs) {
+                field_bounds(me, W);
+                rc = k1_alloc(me.d, M, W - M, lane, e, rounds);
+            }
+            if (rc == K1_INFEASIBLE) {
+                st = HALDA_STATUS_INFEASIBLE;
+            } else if (rc == K1_OK) {
+                double g = 0.0, H = 0.0, z = 0.0;
+                int n = 0, sl[4] = {0, 0, 0, 0};
+                const int wl = 1 + e;
+                if (lane < M) {
+                    double P, Q;
+                    split_full(me.d, wl, g, n, sl);
+                    dev_cycle(me.d, wl, n, sl, P, Q);
+                    z = Q > P ? 0.5 * (Q - P) : 0.0;
+                    H = Q >= P ? 0.5 * (P + Q) : P;
+                }
+                const double hmax = fmax(0.0, wave_max(lane < M ? H : 0.0));
+                obj = wave_sum_f64(lane < M ? g : 0.0) + kc * hmax;
+                obj = obj + tsum;
+                obj = obj + xsum;
+                obj = obj + kappa;
+                st = HALDA_STATUS_OPTIMAL;
+                improved = obj < best;
+                if (lane < M) {
+                    put_xc(A, inst, M, lane, wl, n, sl, z, me.d);
+                    if (improved) {
+                        A.out.w[d0 + lane] = wl;
+                        A.out.n[d0 + lane] = n;
+                    }
+                }
+                if (lane == 0) {
+                    if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
+                    if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
+                }
+            } else if constexpr (!kTables) {
+                // k > 1, a wide fleet or a fast-path fallback: the table launch redoes this fleet
+                if (lane == 0) {
+                    A.fflag[f] = 1;
+                    __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                return;
+            } else {
+                Inst I = {};
+                I.M = M;
+                I.W = W;
+                I.Wd = double(W);
+                I.kc = kc;
+                I.iC = 7 * M;
+                I.R1 = W - M + 1;
+                I.RS = odd_stride(I.R1);
+                const FieldSrc src{&A.Mo, &A.F, d0, W};
+                int64_t nodes = 0;
+                if (M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab)) {
+                    st = HALDA_STATUS_TOO_LARGE;  // beyond the launch's slice (the host sizes it from the fleets)
+                } else if (table_pass(src, w, I, lane), wave_sync(), !dp_pass(w, I, lane, nodes)) {
+                    st = HALDA_STATUS_INFEASIBLE;
+                } else {
+                    // solution: per device (w, n, least slacks, z), sum of costs, largest cycle time
+                    double gs = 0.0, hmax = 0.0;
+                    for (int i = lane; i < M; i += 64) {
+                        Dev d;
+                        src.load(d, w, i);
+                        const int wl = 1 + w.st0[i];
+                        double g = 0.0, P, Q;
+                        int n = 0, sl[4] = {0, 0, 0, 0};
+                        split_full(d, wl, g, n, sl);
+                        dev_cycle(d, wl, n, sl, P, Q);
+                        gs += g;
+                        hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
+                        put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
+                    }
+                    hmax = wave_max(hmax);
+                    obj = wave_sum_f64(gs) + kc * hmax;
+                    obj = obj + tsum;
+                    obj = obj + xsum;
+                    obj = obj + kappa;
+                    st = HALDA_STATUS_OPTIMAL;
+                    improved = obj < best;
+                    if (improved)
+                        for (int i = lane; i < M; i += 64) {
+                            Dev d;
+                            src.load(d, w, i);
+                            const int wl = 1 + w.st0[i];
+                            double g;
+                            int n = 0, sl[4];
+                            split_full(d, wl, g, n, sl);
+                            A.out.w[d0 + i] = wl;
+                            A.out.n[d0 + i] = n;
+                        }
+                    if (lane == 0) {
+                        if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
+                        if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
+                    }
+                }
+                wave_sync();  // tables / st0 are rewritten by the next k
+            }
+        }
+        if (st == HALDA_STATUS_OPTIMAL && M == 0) {
+            obj = 0.0;  // c.x = 0; no devices: the offsets are empty sums and kappa is undefined
+            improved = obj < best;
+            if (lane == 0) {
+                if (A.out.x) A.out.x[inst * A.xstride] = 0.0;
+                if (A.out.c) A.out.c[inst * A.xstride] = kc;
+            }
+        }
+        if (improved) {
+            best = obj;
+            best_k = k;
+        }
+        if (st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
+            const int N = 7 * M + 1;
+            for (int cc = lane; cc < N; cc += 64) {
+                if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
+                if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
+            }
+        }
+        if (lane == 0) {
+            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.out.status) A.out.status[inst] = st;
+        }
+    }
+    if (lane == 0) {
+        A.out.best_k[f] = best_k;
+        A.out.obj_value[f] = best;
+        if (!kTables) A.fflag[f] = 0;
+    }
+    if (best_k == 0)
+        for (int i = lane; i < M; i += 64) {
+            A.out.w[d0 + i] = 0;
+            A.out.n[d0 + i] = 0;
+        }
+}
+
+template <bool kTables, bool kGlobal>
+__device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base) {
+    const int lane = threadIdx.x;
+    if (A.want == 1 && __hip_atomic_load(A.hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.launch_id)
+        return;
+    WaveCtx w = {};
+    if constexpr (kTables) {
+        const Slice sl = make_slice(A.mmax, A.r1max, A.tab, A.tab_kc);
+        unsigned char *base = slice_base;
+        w.rows = reinterpret_cast<int2 *>(base + sl.rows);
+        w.cyc = reinterpret_cast<double *>(base + sl.cyc);
+        w.cost = reinterpret_cast<double *>(base + sl.cost);
+        w.cnt = reinterpret_cast<int *>(base + sl.cnt);
+        w.st0 = reinterpret_cast<int *>(base + sl.st0);
+        w.st1 = reinterpret_cast<int *>(base + sl.st1);
+        w.rng = reinterpret_cast<int2 *>(base + sl.rng);
+        w.inc = reinterpret_cast<double *>(base + sl.inc);
+        w.G = reinterpret_cast<double *>(base + sl.G);
+        w.H = reinterpret_cast<double *>(base + sl.H);
+        w.work = reinterpret_cast<double *>(base + sl.work);
+        w.split = reinterpret_cast<uint16_t *>(base + sl.split);
+    }
+    const int S = gridDim.x;
+    const int nf = A.F.n_fleets;
+    for (int64_t b = blockIdx.x; b < nf; b += int64_t(64) * S) {
+        const int64_t mine = b + int64_t(lane) * S;
+        uint64_t todo = __ballot(mine < nf && (A.want == 0 || A.fflag[mine] == 1));
+        while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            sweep_fleet<kTables, kGlobal>(A, int(b + int64_t(bit) * S), w, lane);
+        }
+    }
+}
+
+#ifndef HALDA_SWEEP_WAVES_PER_SIMD
+#define HALDA_SWEEP_WAVES_PER_SIMD 4  // occupancy target of the register-only sweep (as the k = 1 kernel)
+#endif
+
+__global__ __launch_bounds__(64, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_kernel(SweepArgs A) {
+    sweep_body<false, false>(A, nullptr);
+}
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    sweep_body<true, false>(A, smem);
+}
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_big_kernel(SweepArgs A) {
+    sweep_body<true, true>(A, A.gtab + int64_t(blockIdx.x) * A.gstride);
 }
 
 // halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
@@ -2473,6 +2856,12 @@ struct Ctx {
     void *gtab = nullptr;  // per-wave global-memory slices of the big-table general launch
     size_t gtab_bytes = 0;
     hipEvent_t ev_order = nullptr;  // cross-stream ordering of consecutive launches on this context
+    hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around a halda_solve_fleets sequence (lowering .. pick)
+    bool fleet_timed = false;
+    bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
+    bool last_fleet_fused = false;
+    void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
+    size_t fflag_bytes = 0;
     hipStream_t last_stream = nullptr;
     bool have_last = false;
     void *fleet_scratch = nullptr;  // lowered batch + results of halda_solve_fleets
@@ -2665,6 +3054,101 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     return HALDA_OK;
 }
 
+// Fused k-sweep (halda_sweep_kernel): one register-only launch over every fleet, then the table
+// launch for the fleets it flagged (gated on the hand-back flag); a batch whose k > 1 / wide
+// fleets need tables from the start gets the table launch only (LDS slice), or, beyond the LDS
+// budget, the register launch plus the global-table launch.
+int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
+                 const halda_fleet_result &out, hipStream_t s) {
+    const int nf = F.n_fleets;
+    int64_t r1_k1 = 0, r1_kc = 0;
+    for (int j = 0; j < n_k; ++j) {
+        const int64_t r1 = int64_t(model.L / kh[j]) - F.min_devices + 1;
+        if (kh[j] == 1) r1_k1 = std::max(r1_k1, r1);
+        else r1_kc = std::max(r1_kc, r1);
+    }
+    const int mmax = F.max_devices;
+    const int64_t r1max = std::max<int64_t>(1, std::max(r1_k1, r1_kc));
+    // table sizes in doubles (odd row stride: at most one extra double per device)
+    const int64_t tab = r1_k1 > 0 ? int64_t(mmax) * r1_k1 + mmax : 1;
+    const int64_t tab_kc = r1_kc > 0 ? int64_t(mmax) * r1_kc + mmax : 0;
+    if (r1max > kMaxR1 || tab > (1 << 27) || tab_kc > (1 << 27))
+        return fail(HALDA_E_ARG, "fleet shape out of range: (L / k_min - min_devices + 1) * max_devices > 2^27");
+    const bool tables_first = tab_kc > 0 || mmax > kK1MaxM;
+    const int64_t slice = make_slice(mmax, int(r1max), int(tab), int(tab_kc)).total;
+    const bool fits = slice <= kLdsBudget;
+    // staging: ks and the per-fleet flags
+    const size_t need = 256 + ((size_t(nf) + 255) & ~size_t(255));
+    if (need > c->fflag_bytes) {
+        if (c->fflag) HIP_TRY(hipFree(c->fflag));
+        c->fflag = nullptr;
+        c->fflag_bytes = 0;
+        HIP_TRY(hipMalloc(&c->fflag, need));
+        c->fflag_bytes = need;
+    }
+    int32_t *ks_dev = static_cast<int32_t *>(c->fflag);
+    HIP_TRY(hipMemcpyAsync(ks_dev, kh, sizeof(int32_t) * size_t(n_k), hipMemcpyHostToDevice, s));
+    SweepArgs A = {};
+    A.Mo = model;
+    A.F = F;
+    A.ks = ks_dev;
+    A.n_k = n_k;
+    A.out = out;
+    A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
+    A.fflag = static_cast<uint8_t *>(c->fflag) + 256;
+    A.hb_flag = c->hb_flag;
+    A.launch_id = ++c->launch_id;
+    A.mmax = mmax;
+    A.r1max = int(r1max);
+    A.tab = int(tab);
+    A.tab_kc = int(tab_kc);
+    c->fleet_timed = false;
+    c->have_lowered = false;
+    if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
+    if (tables_first && fits) {
+        int per_cu = 0;
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
+        A.want = 0;
+        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
+        HIP_TRY(hipGetLastError());
+    } else {
+        A.want = 0;
+        hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned(nf)), dim3(64), 0, s, A);
+        HIP_TRY(hipGetLastError());
+        A.want = 1;  // the fleets flagged above, gated on the hand-back flag
+        if (fits) {
+            int per_cu = 0;
+            HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
+            const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
+            hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
+        } else {
+            A.gstride = (slice + 255) & ~int64_t(255);
+            int per_cu = 0;
+            HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_big_kernel), 0, &per_cu));
+            const int grid = int(std::max<int64_t>(
+                1, std::min<int64_t>({int64_t(c->cus) * per_cu, int64_t(nf), kGlobalTableBudget / A.gstride})));
+            const size_t gneed = size_t(A.gstride) * size_t(grid);
+            if (gneed > c->gtab_bytes) {
+                if (c->gtab) HIP_TRY(hipFree(c->gtab));
+                c->gtab = nullptr;
+                c->gtab_bytes = 0;
+                HIP_TRY(hipMalloc(&c->gtab, gneed));
+                c->gtab_bytes = gneed;
+            }
+            A.gtab = static_cast<unsigned char *>(c->gtab);
+            hipLaunchKernelGGL(halda_sweep_big_kernel, dim3(grid), dim3(64), 0, s, A);
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    if (c->timing) {
+        HIP_TRY(hipEventRecord(c->evf1, s));
+        c->fleet_timed = true;
+    }
+    c->last_fleet_fused = true;
+    return HALDA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2705,12 +3189,15 @@ int halda_init(int device_ordinal, void **ctx_out) {
     }
     const char *tp = std::getenv("HALDA_TWO_PASS");
     c->two_pass = !(tp && tp[0] == '0');
+    const char *fp = std::getenv("HALDA_FLEETS_PATH");
+    c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&c->evf0) != hipSuccess || hipEventCreate(&c->evf1) != hipSuccess) {
         halda_free(c);
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
@@ -2728,7 +3215,10 @@ void halda_free(void *ctx) {
     if (c->hb_flag) (void)hipFree(c->hb_flag);
     if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
     if (c->gtab) (void)hipFree(c->gtab);
+    if (c->fflag) (void)hipFree(c->fflag);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    if (c->evf0) (void)hipEventDestroy(c->evf0);
+    if (c->evf1) (void)hipEventDestroy(c->evf1);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evs) (void)hipEventDestroy(c->evs);
@@ -2790,6 +3280,40 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
     return HALDA_OK;
 }
 
+int halda_set_fleets_path(void *ctx, int fused) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c) return fail(HALDA_E_ARG, "NULL ctx");
+    c->fleets_fused = fused != 0;
+    return HALDA_OK;
+}
+
+int halda_last_fleet_ms(void *ctx, double *ms6) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !ms6) return fail(HALDA_E_ARG, "NULL ctx/ms");
+    if (!c->fleet_timed) return fail(HALDA_E_ARG, "no timed halda_solve_fleets call on this context");
+    HIP_TRY(hipEventSynchronize(c->evf1));
+    if (c->last_fleet_fused) {
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, c->evf0, c->evf1));
+        ms6[0] = t;
+        for (int i = 1; i < 6; ++i) ms6[i] = 0.0;
+        return HALDA_OK;
+    }
+    float lo = 0.f, a = 0.f, b = 0.f, d = 0.f, pk = 0.f;
+    HIP_TRY(hipEventElapsedTime(&lo, c->evf0, c->ev0));
+    HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evk));
+    HIP_TRY(hipEventElapsedTime(&b, c->evk, c->evs));
+    HIP_TRY(hipEventElapsedTime(&d, c->evs, c->ev1));
+    HIP_TRY(hipEventElapsedTime(&pk, c->ev1, c->evf1));
+    ms6[0] = 0.0;
+    ms6[1] = lo;
+    ms6[2] = a;
+    ms6[3] = b;
+    ms6[4] = d;
+    ms6[5] = pk;
+    return HALDA_OK;
+}
+
 #ifdef HALDA_STAMPS
 int halda_debug_stamps(unsigned long long *out, int n_inst) {
     const int n = std::min(n_inst, kStampInst);
@@ -2824,6 +3348,7 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
         const int rc = order_after_previous(c, s);  // fleet_scratch / last_lowered are per context
         if (rc != HALDA_OK) return rc;
     }
+    if (c->fleets_fused && n_k <= 64) return sweep_fleets(c, *model, F, ks, n_k, *out, s);
     const LowerDims D = lower_dims(F.max_devices, n_k);
     const int64_t n_inst = int64_t(F.n_fleets) * n_k;
     if (n_inst > (int64_t(1) << 30) || int64_t(F.n_fleets) * D.nnz > (int64_t(1) << 31) - 1)
@@ -2867,6 +3392,9 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     O.row_ub = reinterpret_cast<double *>(base + o_rub);
     O.integrality = reinterpret_cast<uint8_t *>(base + o_int);
     O.offs = reinterpret_cast<double *>(base + o_offs);
+    c->fleet_timed = false;
+    c->last_fleet_fused = false;
+    if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
     hipLaunchKernelGGL(halda_lower_kernel, dim3(unsigned(F.n_fleets)), dim3(64), 0, s, *model, F, ks_dev, int(n_k), D,
                        O);
     HIP_TRY(hipGetLastError());
@@ -2916,6 +3444,10 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     hipLaunchKernelGGL(halda_pick_kernel, dim3(unsigned(F.n_fleets)), dim3(64), 0, s, b, r, F, int(n_k),
                        static_cast<const double *>(O.offs), *out, D.cols);
     HIP_TRY(hipGetLastError());
+    if (c->timing) {
+        HIP_TRY(hipEventRecord(c->evf1, s));
+        c->fleet_timed = true;
+    }
     c->last_lowered = b;
     c->last_solved = r;
     c->have_lowered = true;
@@ -3018,7 +3550,9 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
 int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c || !lowered || !solved) return fail(HALDA_E_ARG, "NULL ctx/lowered/solved");
-    if (!c->have_lowered) return fail(HALDA_E_ARG, "no halda_solve_fleets call on this context");
+    if (!c->have_lowered)
+        return fail(HALDA_E_ARG, "no lowered batch: the last halda_solve_fleets call ran the fused sweep "
+                                 "(halda_set_fleets_path(ctx, 0) selects the CSR pipeline)");
     *lowered = c->last_lowered;
     *solved = c->last_solved;
     return HALDA_OK;

@@ -76,7 +76,8 @@ class HaldaResultC(ctypes.Structure):
 
 EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
            "halda_last_solve_kernel_ms", "halda_last_phase_ms", "halda_lds_bytes", "halda_last_error", "halda_free",
-           "halda_solve_fleets", "halda_solve_fleets_host", "halda_last_lowered", "halda_set_timing")
+           "halda_solve_fleets", "halda_solve_fleets_host", "halda_last_lowered", "halda_set_timing",
+           "halda_last_fleet_ms", "halda_set_fleets_path")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -107,6 +108,10 @@ def load_library(path: Path | str | None = None):
         lib.halda_last_solve_kernel_ms.restype = ctypes.c_int
         lib.halda_last_phase_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.halda_last_phase_ms.restype = ctypes.c_int
+        lib.halda_set_fleets_path.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.halda_set_fleets_path.restype = ctypes.c_int
+        lib.halda_last_fleet_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        lib.halda_last_fleet_ms.restype = ctypes.c_int
         lib.halda_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.halda_set_timing.restype = ctypes.c_int
         lib.halda_lds_bytes.argtypes = [ctypes.c_int32] * 4
@@ -240,8 +245,9 @@ class HaldaContext:
         s.mip_rel_gap = b.mip_rel_gap
         s.time_limit = 3600.0
         r = HaldaResultC(**{k: int(v) for k, v in out_ptrs.items()})
-        rc = self.lib.halda_solve_batch_device(self.ctx, ctypes.byref(s), ctypes.byref(r),
-                                               ctypes.c_void_p(stream) if stream else None)
+        with self._lock:  # one launch at a time per context (verdict bytes, hand-back flag)
+            rc = self.lib.halda_solve_batch_device(self.ctx, ctypes.byref(s), ctypes.byref(r),
+                                                   ctypes.c_void_p(stream) if stream else None)
         if rc != 0:
             raise RuntimeError(f"halda_solve_batch_device failed ({rc}): {last_error(self.lib)}")
 
@@ -254,9 +260,23 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
+    def set_fleets_path(self, fused: bool) -> None:
+        """halda_solve_fleets on the fused sweep (True, default) or the CSR pipeline (False)."""
+        self.lib.halda_set_fleets_path(self.ctx, int(bool(fused)))
+
     def set_timing(self, on: bool) -> None:
         """Record (or not) the per-launch HIP events behind last_kernel_ms / last_phase_ms."""
         self.lib.halda_set_timing(self.ctx, int(bool(on)))
+
+    def last_fleet_ms(self) -> Dict[str, float]:
+        """Device time of each launch of the last halda_solve_fleets call (zero entries dropped)."""
+        ms = (ctypes.c_double * 6)()
+        rc = self.lib.halda_last_fleet_ms(self.ctx, ms)
+        if rc != 0:
+            raise RuntimeError(f"halda_last_fleet_ms failed ({rc}): {last_error(self.lib)}")
+        names = ("halda_sweep_kernel", "halda_lower_kernel", "halda_screen_kernel", "halda_solve_k1_kernel",
+                 "halda_solve_kernel", "halda_pick_kernel")
+        return {n: float(v) for n, v in zip(names, ms) if v > 0.0}
 
     def last_phase_ms(self) -> Dict[str, float]:
         """Device time of each launch of the last solve: screen, k = 1 fast path, general kernel."""

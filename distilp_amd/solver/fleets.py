@@ -1,8 +1,9 @@
 """Whole k-sweeps on the GPU from a flat device-field table (libhalda `halda_solve_fleets`).
 
-`halda_solve` (halda.py) keeps the reference's host lowering so its objective is
-formed by NumPy exactly as the reference forms it. This module is the
-throughput / streaming path above the same kernels: fleets are packed into a
+`halda_solve` (halda.py) runs one fleet through this path and forms obj_value from
+the returned c and x with NumPy, exactly as the reference forms it;
+`halda_solve_fleets` below is the throughput / streaming entry on the same
+kernels (obj_value formed on the GPU). Fleets are packed into a
 `FleetTable` (one entry per device, the fields the reference's formulas read,
 dense_common.py:25-230), and libhalda lowers every (fleet, k) on the GPU
 (bit-identical CSR to `lower.lower_fleet`), solves it and keeps the best k by the
@@ -151,34 +152,43 @@ class FleetTable:
                 raise ZeroDivisionError("float division by zero")
 
 
-def _rate(table, q) -> tuple:
-    """(present, value) of sum_f_over_s's S[q]["b_1"] (dense_common.py:49-75)."""
+def _rate(table, q, f_has_b1: bool, raise_on_missing: bool) -> tuple:
+    """(present, value) of _sum_f_over_S's S[q]["b_1"] (dense_common.py:49-75): present when q is in
+    the table with a "b_1" entry. The reference raises ValueError when "b_1" is in f and q is in S
+    but S[q] lacks "b_1" (:62-64); with f lacking "b_1" the term is silently 0."""
     if table is None or q not in table:
         return False, 0.0
     row = table[q]
     if "b_1" not in row:
-        raise ValueError(f"Batch size 1 (key 'b_1') not found in S_by_q[{q}]")
+        if f_has_b1 and raise_on_missing:
+            raise ValueError(f"Batch size 1 (key 'b_1') not found in S_by_q[{q}]")
+        return False, 0.0
     return True, float(row["b_1"])
 
 
 def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
     """Pack fleets (lists of DeviceProfile) into a FleetTable."""
     Q = model.Q
+    fq, fout = "b_1" in model.f_q, "b_1" in model.f_out
     cls, flags, cols = [], [], {f: [] for f in F64_FIELDS + I64_FIELDS}
     off = [0]
     for devs in fleets:
         if not devs:
             raise IndexError("list index out of range")  # the reference's kappa on an empty fleet
-        for d in devs:
+        head = next((i for i, d in enumerate(devs) if d.is_head), 0)  # kappa's head (dense_common.py:214-219)
+        for i, d in enumerate(devs):
             cls.append({"mac_no_metal": 1, "mac_metal": 2}.get(d.os_type, 3))
             fl = (DEV_HEAD if d.is_head else 0) | (DEV_UMA if d.is_unified_mem else 0)
-            ok, v = _rate(d.scpu, Q)
+            # alpha reads scpu with f_q; kappa reads the head's scpu with f_out
+            ok, v = _rate(d.scpu, Q, fq, True)
+            if i == head:
+                _rate(d.scpu, Q, fout, True)
             fl |= DEV_CPU_RATE if ok else 0
             table, tg = gpu_flops_table(d), gpu_load_throughput(d)
             gv, tgv = 0.0, 1.0
             if table is not None and tg is not None:
                 fl |= DEV_GPU
-                gok, gv = _rate(table, Q)
+                gok, gv = _rate(table, Q, fq, True)
                 fl |= DEV_GPU_RATE if gok else 0
                 tgv = float(tg)
             fl |= DEV_CUDA_OK if (d.has_cuda and d.d_avail_cuda is not None) else 0
@@ -300,3 +310,46 @@ def halda_solve_fleets(
         out.append(HALDAResult(w=[int(v) for v in res.w[a:b]], n=[int(v) for v in res.n[a:b]], k=int(res.best_k[f]),
                                obj_value=float(res.obj_value[f]), sets=assign_sets(list(devs))))
     return out
+
+
+class DeviceFleetTable:
+    """A FleetTable resident in device memory (torch tensors) plus device result buffers, for
+    back-to-back asynchronous halda_solve_fleets launches (bench / streaming): nothing crosses PCIe
+    per launch except the k list (n_k int32, staged by the call)."""
+
+    def __init__(self, table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float, torch_device,
+                 want_per_k: bool = False):
+        import torch
+
+        self.table = table
+        self.ks = np.asarray([int(k) for k in ks], np.int32)
+        self.arrs = {f: torch.from_numpy(np.ascontiguousarray(getattr(table, f))).to(torch_device)
+                     for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS}
+        nf, nd, nk = table.n_fleets, table.n_devices, len(self.ks)
+        self.out = {"best_k": torch.empty(nf, dtype=torch.int32, device=torch_device),
+                    "obj_value": torch.empty(nf, dtype=torch.float64, device=torch_device),
+                    "w": torch.empty(nd, dtype=torch.int32, device=torch_device),
+                    "n": torch.empty(nd, dtype=torch.int32, device=torch_device)}
+        if want_per_k:
+            self.out["obj_by_k"] = torch.empty(nf * nk, dtype=torch.float64, device=torch_device)
+            self.out["status"] = torch.empty(nf * nk, dtype=torch.int32, device=torch_device)
+        self.fs = _fleets_struct(table, lambda f: self.arrs[f].data_ptr())
+        o = self.out
+        self.res = HaldaFleetResultC(o["best_k"].data_ptr(), o["obj_value"].data_ptr(), o["w"].data_ptr(),
+                                     o["n"].data_ptr(), o["obj_by_k"].data_ptr() if want_per_k else None,
+                                     o["status"].data_ptr() if want_per_k else None, None, None)
+        self.model = model_struct(model, kv_factor)
+
+    def nbytes(self) -> int:
+        return sum(int(t.numel() * t.element_size()) for t in self.arrs.values())
+
+    def launch(self, ctx, stream: int) -> None:
+        """Enqueue one k-sweep of every fleet on `stream` (a hipStream_t as int)."""
+        lib = _bind(ctx.lib)
+        with ctx._lock:
+            rc = lib.halda_solve_fleets(ctx.ctx, ctypes.byref(self.model), ctypes.byref(self.fs),
+                                        self.ks.ctypes.data, len(self.ks), ctypes.byref(self.res),
+                                        ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"halda_solve_fleets failed ({rc}): {last_error(lib)}")
+

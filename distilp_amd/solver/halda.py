@@ -19,7 +19,7 @@ host restatement pinned to the reference's arrays) and solved exactly (gap 0)
 in ONE halda_solve_fleets call, instead of one scipy/HiGHS call per k. The
 objective of each k is then formed here with NumPy from the returned c and x,
 exactly as the reference forms it. `halda_solve_batch` keeps the host lowering
-(one CSR per fleet shared by its k-instances through `halda_solve_batch`).
+(one CSR per fleet shared by its k-instances through the C-ABI halda_solve_batch).
 """
 
 from __future__ import annotations
@@ -73,38 +73,52 @@ def _offset_parts(devs, model: ModelProfile, sets) -> Tuple[float, float, float]
     return t_comm, xi_sum, kappa
 
 
-def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: float, offsets,
-                  device: int) -> List[Tuple[int, Optional[ILPResult]]]:
+def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: float, device: int,
+                  debug: bool) -> List[Tuple[int, Optional[ILPResult]]]:
     """Every k of one fleet lowered, solved and returned by ONE halda_solve_fleets call (the CSR is
     built on the GPU, bit-identical to lower.lower_fleet); obj_value = c.x + offsets formed here with
-    NumPy on the returned c and x, exactly as the reference forms it (halda_p_solver.py:347-357)."""
-    if any(k == 0 for k in Ks):
-        raise ZeroDivisionError("integer division or modulo by zero")  # W = L // k (halda_p_solver.py:76)
+    NumPy on the returned c and x, exactly as the reference forms it (halda_p_solver.py:347-357).
+
+    Errors surface where the reference's k loop (halda_p_solver.py:391-412) raises them: k = 0 at
+    W = L // k (:72), then the k-independent coefficient errors (b_1 missing, zero T_cpu / s_disk,
+    empty fleet) at the first k, after that k's debug line."""
+    try:
+        offsets = _offset_parts(devs, model, sets)
+        table = fleet_table([devs], model)
+        err = None
+    except Exception as e:  # noqa: BLE001 -- re-raised at the first k, as the reference raises it
+        err = e
     pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
-    table = fleet_table([devs], model)
-    res = solve_table(table, model, pos, kv_factor, device, want_x=True) if pos else None
     M, N = len(devs), 7 * len(devs) + 1
-    t_comm, xi_sum, kappa = offsets
+    res = None
     out: List[Tuple[int, Optional[ILPResult]]] = []
     for k in Ks:
-        if k < 0:
-            out.append((k, None))
-            continue
-        j = pos.index(k)
-        st = int(res.status[0, j])
-        if st == STATUS_OPTIMAL:
-            x = np.array(res.x[0, j, :N])
-            c = np.array(res.c[0, j, :N])
-            obj = float(c.dot(x)) + t_comm + xi_sum + kappa
-            out.append((k, ILPResult(k=k, w=[int(round(v)) for v in x[:M]], n=[int(round(v)) for v in x[M:2 * M]],
-                                     obj_value=obj)))
-        elif st == STATUS_INFEASIBLE:
-            out.append((k, None))
-        else:
-            raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
-                               "the lowered MILP does not have the HALDA structure")
+        if debug:
+            print("k: " + str(k))
+        if k == 0:
+            raise ZeroDivisionError("integer division or modulo by zero")
+        if err is not None:
+            raise err
+        r: Optional[ILPResult] = None
+        if k > 0:
+            if res is None:
+                res = solve_table(table, model, pos, kv_factor, device, want_x=True)
+            j = pos.index(k)
+            st = int(res.status[0, j])
+            if st == STATUS_OPTIMAL:
+                x = np.array(res.x[0, j, :N])
+                c = np.array(res.c[0, j, :N])
+                t_comm, xi_sum, kappa = offsets
+                obj = float(c.dot(x)) + t_comm + xi_sum + kappa
+                r = ILPResult(k=k, w=[int(round(v)) for v in x[:M]], n=[int(round(v)) for v in x[M:2 * M]],
+                              obj_value=obj)
+            elif st != STATUS_INFEASIBLE:
+                raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
+                                   "the lowered MILP does not have the HALDA structure")
+        out.append((k, r))
+        if debug:
+            print(f"  k={k:<4d}  obj=infeasible" if r is None else f"  k={k:<4d}  obj={r.obj_value:.6f}")
     return out
-
 
 
 def _pick(per_k: List[Tuple[int, Optional[ILPResult]]]) -> Optional[ILPResult]:
@@ -130,17 +144,9 @@ def halda_solve(
     kv_factor = kv_bits_to_factor(kv_bits)
     devs = list(devs)
     sets = assign_sets(devs)
-    offsets = _offset_parts(devs, model, sets)  # raises the reference's errors on degenerate fleets
-    per_k = _sweep_on_gpu(devs, model, sets, Ks, kv_factor, offsets, device)
-
     if debug:
         print("Objectives by k")
-        for k, r in per_k:
-            print("k: " + str(k))
-            if r is None:
-                print(f"  k={k:<4d}  obj=infeasible")
-            else:
-                print(f"  k={k:<4d}  obj={r.obj_value:.6f}")
+    per_k = _sweep_on_gpu(devs, model, sets, Ks, kv_factor, device, debug) if Ks else []
     best = _pick(per_k)
     if best is None:
         raise RuntimeError("No feasible MILP found for any k this round.")

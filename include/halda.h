@@ -189,9 +189,23 @@ typedef struct halda_fleet_result {
 
 /* Asynchronous on `stream` (NULL = the context's stream): the halda_fleets and
  * halda_fleet_result arrays are device memory; ks (host memory, n_k entries)
- * is ascending, unique, > 0. Shape limits: L / ks[0] - min_devices + 1 <= 128. */
+ * is ascending, unique, > 0 (at most 64 entries on the fused path). Shape limit:
+ * (L / ks[0] - min_devices + 1) * max_devices <= 2^27; tables beyond the LDS budget go to HBM. */
 int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                        int32_t n_k, halda_fleet_result *out, void *stream);
+
+/* How halda_solve_fleets runs (default 1, or 0 when HALDA_FLEETS_PATH=csr is set at halda_init):
+ * 1 the fused sweep (halda_sweep_kernel: every (fleet, k) built in registers from the device
+ *   fields, solved and compared in one wave per fleet; no MILP is materialised);
+ * 0 the CSR pipeline (lowering kernel -> the halda_solve_batch kernels -> pick kernel), which also
+ *   keeps the lowered batch for halda_last_lowered. Both give the same statuses, x and k. */
+int halda_set_fleets_path(void *ctx, int fused);
+
+/* Device time of the last halda_solve_fleets call per launch, in ms (per-launch events on, see
+ * halda_set_timing): ms6[0] the fused sweep kernel (0 when the CSR pipeline ran), ms6[1] the lowering
+ * kernel, ms6[2] the screen, ms6[3] the k = 1 solve, ms6[4] the general kernel's launches, ms6[5] the
+ * pick kernel. */
+int halda_last_fleet_ms(void *ctx, double *ms6);
 
 /* Synchronous variant on HOST arrays (halda_fleets / halda_fleet_result in host
  * memory; obj_by_k and status may be NULL). */

@@ -1,6 +1,7 @@
-"""GPU k-sweeps from a device-field table (libhalda halda_solve_fleets): the GPU lowering is
-bit-identical to the host lowering (itself pinned to the reference's arrays by test_lowering), and
-the per-fleet results equal the host-lowered path's and the reference goldens."""
+"""GPU k-sweeps from a device-field table (libhalda halda_solve_fleets): the GPU lowering of the
+CSR pipeline is bit-identical to the host lowering (itself pinned to the reference's arrays by
+test_lowering), and the per-fleet results of the default fused sweep equal the host-lowered
+path's and the reference goldens."""
 
 import ctypes
 
@@ -46,8 +47,13 @@ def test_gpu_lowering_is_bit_identical(llama_online_model, M, seeds):
     fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)] for s in seeds]
     ks = KS80 + [3, 7]
     ks = sorted(set(ks))
-    solve_table(fleet_table(fleets, llama_online_model), llama_online_model, ks, 0.5)
-    b = _lowered()
+    ctx = get_context(0)
+    ctx.set_fleets_path(False)  # the CSR pipeline keeps the lowered batch (the fused sweep has none)
+    try:
+        solve_table(fleet_table(fleets, llama_online_model), llama_online_model, ks, 0.5)
+        b = _lowered()
+    finally:
+        ctx.set_fleets_path(True)
     n = b.n_inst
     n_cols, n_rows = _d2h(b.n_cols, n, np.int32), _d2h(b.n_rows, n, np.int32)
     csr_off, col_off, row_off = (_d2h(getattr(b, f), n, np.int64) for f in ("csr_off", "col_off", "row_off"))

@@ -1,0 +1,85 @@
+"""The fused k-sweep (halda_sweep_kernel, the default halda_solve_fleets path) against the CSR
+pipeline (GPU lowering -> screen / k = 1 / general kernels -> pick) on the same fleet tables.
+
+The sweep builds each device's record from the fleet table with the coefficient code the lowering
+kernel writes into the CSR, so the two paths must agree on every status, on (w, n) of every
+optimal instance up to exact ties of the objective, on best k / w / n, and on obj_value within
+1e-12 (the fused path sums c.x in another fixed order). Reference: halda_p_solver.py:59-436."""
+
+import numpy as np
+import pytest
+
+from distilp_amd.common import DeviceProfile
+from distilp_amd.solver._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL, STATUS_UNSUPPORTED, get_context
+from distilp_amd.solver.fleets import fleet_table, solve_table
+from distilp_amd.synth import synth_fleet
+
+pytestmark = pytest.mark.gpu
+
+
+def _both(table, model, ks):
+    ctx = get_context(0)
+    fused = solve_table(table, model, ks, 0.5, want_x=True)
+    ctx.set_fleets_path(False)
+    try:
+        csr = solve_table(table, model, ks, 0.5, want_x=True)
+    finally:
+        ctx.set_fleets_path(True)
+    return fused, csr
+
+
+def _compare(table, fused, csr, ks):
+    assert np.array_equal(fused.status, csr.status)
+    assert np.array_equal(fused.best_k, csr.best_k)
+    for f in range(table.n_fleets):
+        M = int(table.dev_off[f + 1] - table.dev_off[f])
+        N = 7 * M + 1
+        for j in range(len(ks)):
+            if csr.status[f, j] != STATUS_OPTIMAL:
+                assert np.isinf(fused.obj_by_k[f, j])
+                continue
+            a, b = fused.obj_by_k[f, j], csr.obj_by_k[f, j]
+            assert abs(a - b) <= 1e-12 * max(1.0, abs(b)), (f, ks[j], a, b)
+            assert np.array_equal(fused.c[f, j, :N], csr.c[f, j, :N])
+            xa, xb = fused.x[f, j, :N], csr.x[f, j, :N]
+            if not np.array_equal(xa[:2 * M], xb[:2 * M]):  # only an exact tie may pick another optimum
+                ca = float(np.dot(csr.c[f, j, :N], xa))
+                cb = float(np.dot(csr.c[f, j, :N], xb))
+                assert abs(ca - cb) <= 1e-12 * max(1.0, abs(cb)), (f, ks[j])
+    assert np.array_equal(fused.w, csr.w) and np.array_equal(fused.n, csr.n)
+    ok = fused.best_k > 0
+    assert np.allclose(fused.obj_value[ok], csr.obj_value[ok], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("L,M,n", [(80, 1, 24), (80, 2, 24), (80, 3, 16), (80, 5, 16), (80, 16, 16),
+                                   (80, 64, 64), (256, 8, 6), (160, 100, 2), (64, 24, 8)])
+def test_fused_sweep_equals_csr_pipeline(llama_online_model, L, M, n):
+    model = llama_online_model.model_copy(update={"L": L})
+    ks = [d for d in range(1, L) if L % d == 0][:12]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(7000 + s, M)] for s in range(n)]
+    table = fleet_table(fleets, model)
+    fused, csr = _both(table, model, ks)
+    _compare(table, fused, csr, ks)
+
+
+def test_fused_sweep_mixed_fleet_sizes(llama_online_model):
+    """One table with fleets of 1..70 devices (tables for k > 1 and for the 70-device fleet)."""
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(8000 + s, M)]
+              for s, M in enumerate([1, 70, 2, 33, 64, 5, 12, 3])]
+    table = fleet_table(fleets, llama_online_model)
+    fused, csr = _both(table, llama_online_model, ks)
+    _compare(table, fused, csr, ks)
+
+
+def test_fused_sweep_rejects_what_decode_rejects(llama_online_model):
+    """A capacity row whose least slack is beyond 1e8 layers is not decoded by the CSR path
+    (UNSUPPORTED); the fused sweep rejects the same instances, bound-infeasible k stay INFEASIBLE."""
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(3, 6)]
+    devs[1] = devs[1].model_copy(update={"d_avail_ram": -(10 ** 18)})  # a linux (M3) device
+    table = fleet_table([devs], llama_online_model)
+    fused, csr = _both(table, llama_online_model, ks)
+    assert np.array_equal(fused.status, csr.status)
+    W = [80 // k for k in ks]
+    assert [int(s) for s in fused.status[0]] == [STATUS_UNSUPPORTED if w >= 6 else STATUS_INFEASIBLE for w in W]

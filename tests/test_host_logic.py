@@ -92,3 +92,53 @@ def test_fixture_device_schema_roundtrip():
         again = DeviceProfile.model_validate_json(d.model_dump_json())
         assert again == d
     assert math.isclose(model.b_layer, 454557696)
+
+
+def _raises(fn):
+    try:
+        fn()
+    except Exception as e:  # noqa: BLE001
+        return type(e)
+    return None
+
+
+@pytest.mark.parametrize("f_q_b1,f_out_b1,head", [(True, True, 0), (False, True, 0), (False, True, 1),
+                                                  (True, False, 1), (False, False, 0)])
+def test_fleet_table_b1_rule_matches_reference(llama_online_model, f_q_b1, f_out_b1, head):
+    """_sum_f_over_S raises only when "b_1" is in f AND q is in S AND S[q] lacks "b_1"
+    (dense_common.py:62-64): alpha reads f_q with every device's scpu, kappa f_out with the head's.
+    fleet_table must raise exactly when the host restatement (coefficients.py) does."""
+    from distilp_amd.solver.fleets import fleet_table
+
+    model = llama_online_model.model_copy(update={
+        "f_q": {} if not f_q_b1 else dict(llama_online_model.f_q),
+        "f_out": {} if not f_out_b1 else dict(llama_online_model.f_out)})
+    devs = [d.model_copy(update={"is_head": False}) for d in synth_devices(3, 0)]
+    devs[head] = devs[head].model_copy(update={"is_head": True})
+    devs[head] = devs[head].model_copy(update={"scpu": {model.Q: {"b_2": 1e11}}})
+    sets = co.assign_sets(devs)
+
+    def host():
+        co.objective_vectors(devs, model, sets, 0.5)
+        co.kappa_constant(devs, model, sets)
+
+    assert _raises(lambda: fleet_table([devs], model)) == _raises(host)
+
+
+def test_halda_solve_raises_where_the_reference_loop_does(llama_online_model, capsys):
+    """k = 0 raises at W = L // k (halda_p_solver.py:72) before anything else; an empty k list is
+    RuntimeError (:413-414) without touching the fleet; coefficient errors surface at the first k,
+    after its debug line. None of these reach the GPU."""
+    from distilp_amd.solver import halda_solve
+
+    devs = synth_devices(2, 0)
+    with pytest.raises(ZeroDivisionError):
+        halda_solve(devs, llama_online_model, k_candidates=[0, 1], plot=False)
+    one_layer = llama_online_model.model_copy(update={"L": 1})
+    with pytest.raises(RuntimeError, match="No feasible MILP found for any k this round."):
+        halda_solve([], one_layer, plot=False)  # valid_factors_of_L(1) == []: the empty fleet is never read
+    assert capsys.readouterr().out == "1 []\n"
+    bad = [devs[0].model_copy(update={"scpu": {llama_online_model.Q: {"b_2": 1e11}}}), devs[1]]
+    with pytest.raises(ValueError, match="b_1"):
+        halda_solve(bad, llama_online_model, k_candidates=[-1, 1], plot=False, debug=True)
+    assert capsys.readouterr().out == "Objectives by k\nk: -1\n"
