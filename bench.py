@@ -180,7 +180,7 @@ def usable_cores():
 def run_cpu_baseline(budget_s: float, M: int):
     """All usable cores (one pinned oracle process each, disjoint fleets), then one core alone."""
     cores, quota = usable_cores()
-    per = 64  # fleets prepared per process (more than ~12 s of HiGHS work per core)
+    per = int(budget_s * 40) + 16  # fleets prepared per process (> budget_s of HiGHS work on one core)
 
     def spawn(core, first):
         return subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-baseline-child",
@@ -376,7 +376,7 @@ def main():
     tbytes = DeviceFleetTable(table, model, ks, 0.5, dev).nbytes()
     n_sw = args.copies or max(2, min(32, math.ceil(2 * MALL_BYTES / max(tbytes, 1))))
     sweeps = [DeviceFleetTable(table, model, ks, 0.5, dev) for _ in range(n_sw)]
-    turn = [0]
+    turn = [0, 0]  # per leg: which resident copy the next step reads
 
     def sweep_step():
         sweeps[turn[0] % n_sw].launch(ctx, sref)
@@ -390,8 +390,8 @@ def main():
     cptrs = [({f: t.data_ptr() for f, t in k.items()}, {f: t.data_ptr() for f, t in o.items()}) for k, o in copies]
 
     def solve_step():
-        ptrs, optrs = cptrs[turn[0] % n_so]
-        turn[0] += 1
+        ptrs, optrs = cptrs[turn[1] % n_so]
+        turn[1] += 1
         ctx.solve_device(ptrs, batch, optrs, stream=sref)
 
     setup_s = time.perf_counter() - t_setup
@@ -401,7 +401,7 @@ def main():
         sweep_step()
         solve_step()
     torch.cuda.synchronize(dev)
-    st = copies[0][1]["status"].cpu().numpy()
+    st = copies[(turn[1] - 1) % n_so][1]["status"].cpu().numpy()
     n_opt, n_inf = int((st == 0).sum()), int((st == 2).sum())
     if n_opt + n_inf != batch.n_inst:
         raise RuntimeError(f"unexpected statuses: {np.unique(st, return_counts=True)}")

@@ -1472,9 +1472,19 @@ __device__ inline double shfl_up1(double v, int lane) {
 
 enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
 
+// A device record as the k = 1 greedy sees it: the full Dev (CSR decode) or a compact record
+// expanded on use (fused sweep); bcast(src) = lane src's record on every lane.
+struct FullRec {
+    Dev d;
+    __device__ inline Dev dev() const { return d; }
+    __device__ inline FullRec bcast(int src) const { return FullRec{bcast_dev(d, src)}; }
+};
+
 // Greedy exchange over lazily evaluated convex leaves (lane = device, M <= 64).
 // On K1_OK, e holds the device's extra layers.
-__device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &rounds) {
+template <class Rec>
+__device__ int k1_alloc(const Rec &rec, int M, int R, int lane, int &e, int &rounds) {
+    const Dev d = rec.dev();
     const bool act = lane < M;
     double g0 = kInf, g1 = kInf;
     int n0 = 0, n1 = 0, s[4];
@@ -1506,7 +1516,7 @@ __device__ int k1_alloc(const Dev &d, int M, int R, int lane, int &e, int &round
         bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
         double Gt = kInf, dt = kInf;
         if (need > 1) {
-            const Dev dw = bcast_dev(d, win);
+            const Dev dw = rec.bcast(win).dev();
             const int wl = dw.wlo + ew + 2 + lane;
             double g = kInf;
             int nn = 0;
@@ -1847,7 +1857,7 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_PSTAMP(3);
     HALDA_PSTAMP(4);
     int e = 0, rounds = 0;
-    const int rc = k1_alloc(d, I.M, I.W - sumlo, lane, e, rounds);
+    const int rc = k1_alloc(FullRec{d}, I.M, I.W - sumlo, lane, e, rounds);
     wave_sync();  // LDS records are rewritten by the next instance
     HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
@@ -2434,39 +2444,65 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
 // per-wave global slice (kGlobal = true); want = 1 selects the flagged fleets only (gated on the
 // hand-back flag), want = 0 every fleet.
 
-// Device record of table entry g for W layers (lb(w) = 1, bounds scaled by W as the lowering
-// writes them); bad = 1 when the lowered rows would be rejected by decode (UNSUPPORTED).
-struct FieldDev {
-    Dev d;
-    int cls, gpu, bad;
+// Device record of table entry g, compact: the five coefficients, the least-slack offsets of its
+// RAM / Metal row and of its VRAM rows, its class and GPU flag; W = L / k is set per k. dev()
+// expands it to exactly the Dev that decoding the lowered CSR gives (load_dev of decode_cap_row /
+// decode_cycle_row output), so the solve code is shared; bad = 1 where decode would reject.
+struct FieldRec {
+    double alpha, b, p_bp, p_b, cst;
+    int Kset, Kvram;  // kNoRow: the row is absent
+    int cls, gpu, W;
+    __device__ inline Dev dev() const {
+        Dev d;
+        d.cw = alpha; d.cn = b; d.cs0 = p_bp; d.cs1 = p_b; d.cs2 = p_bp; d.cs3 = cls == 2 ? p_b : p_bp;
+        // cycle rows: busy + z - C <= -cst, busy + F - z - C <= -cst (w entries alpha, alpha + b'/s_disk)
+        d.r1w = alpha;
+        d.r2w = alpha + p_bp;
+        d.rhs1 = -cst;
+        d.rhs2 = -cst;
+        d.wlo = 1; d.whi = W; d.nlo = 0; d.nhi = gpu ? W : 0;
+        const bool hs = Kset != kNoRow, hv = Kvram != kNoRow;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const bool mine = cls == j + 1;
+            d.slo[j] = 0;
+            d.shi[j] = mine ? W : 0;
+            d.us[j] = mine && hs ? 1 : 0;
+            d.vs[j] = j == 2 && mine && hs ? -1 : 0;
+            d.Ks[j] = mine ? Kset : kNoRow;
+        }
+        d.slo[3] = 0; d.shi[3] = gpu ? W : 0; d.us[3] = 0; d.vs[3] = hv ? 1 : 0; d.Ks[3] = Kvram;
+        // the link row n - w <= 0 (scale 1: K = floor(0 + 1e-9) = 0)
+        d.uf[0] = -1; d.vf[0] = 1; d.Kf[0] = 0;
+        d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
+        return d;
+    }
+    __device__ inline FieldRec bcast(int src) const {
+        FieldRec o;
+        o.alpha = ::bcast(alpha, src); o.b = ::bcast(b, src); o.p_bp = ::bcast(p_bp, src);
+        o.p_b = ::bcast(p_b, src); o.cst = ::bcast(cst, src);
+        o.Kset = ::bcast(Kset, src); o.Kvram = ::bcast(Kvram, src);
+        const int cg = ::bcast(cls | (gpu << 4), src);
+        o.cls = cg & 15; o.gpu = cg >> 4;
+        o.W = W;
+        return o;
+    }
 };
 
-__device__ inline FieldDev field_dev(const halda_model &Mo, const halda_fleets &F, int64_t g) {
-    FieldDev o;
+__device__ inline FieldRec field_rec(const halda_model &Mo, const halda_fleets &F, int64_t g, int &bad) {
+    FieldRec r;
     const DevCoef c = dev_coef(Mo, F, g);
     const double bp = Mo.b_prime;
     const uint8_t fl = F.flags[g];
-    o.cls = F.os_class[g];
-    o.gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1 : 0;
-    Dev &d = o.d;
-    d.cw = c.alpha; d.cn = c.b; d.cs0 = c.p_bp; d.cs1 = c.p_b; d.cs2 = c.p_bp; d.cs3 = c.p_v;
-    // cycle rows: busy + z - C <= -cst, busy + F - z - C <= -cst (w entries alpha, alpha + b'/s_disk)
-    d.r1w = c.alpha;
-    d.r2w = c.alpha + c.p_bp;
-    d.rhs1 = -c.cst;
-    d.rhs2 = -c.cst;
-    d.wlo = 1; d.whi = 0; d.nlo = 0; d.nhi = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        d.slo[j] = 0; d.shi[j] = 0; d.us[j] = 0; d.vs[j] = 0; d.Ks[j] = kNoRow;
-    }
-    // the link row n - w <= 0 (scale 1: K = floor(0 + 1e-9) = 0)
-    d.uf[0] = -1; d.vf[0] = 1; d.Kf[0] = 0;
-    d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
-    int bad = !(fabs(c.cst) < 1e300);  // cycle-row rhs
-    bad |= !(c.p_bp >= 0.0) || !(c.p_b >= 0.0) || !(c.p_v >= 0.0);  // device_pass: slack prices >= 0
+    r.alpha = c.alpha; r.b = c.b; r.p_bp = c.p_bp; r.p_b = c.p_b; r.cst = c.cst;
+    r.cls = F.os_class[g];
+    r.gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1 : 0;
+    r.W = 0;
+    r.Kset = r.Kvram = kNoRow;
+    bad = !(fabs(c.cst) < 1e300);  // cycle-row rhs
+    bad |= !(c.p_bp >= 0.0) || !(c.p_b >= 0.0) || !(r.cls == 2 ? c.p_b >= 0.0 : c.p_bp >= 0.0);  // slack prices
     // capacity rows b' u w + b' v n - b' s <= rhs -> s >= u w + v n + ceil(-rhs / b' - eps)
-    auto cap = [&](int kind, int u, int v, double rhs) {
+    auto K = [&](double rhs, int &dst) {
         if (!(bp > 0.0) || !(fabs(rhs) < 1e300)) {
             bad = 1;
             return;
@@ -2476,27 +2512,12 @@ __device__ inline FieldDev field_dev(const halda_model &Mo, const halda_fleets &
             bad = 1;
             return;
         }
-        d.us[kind] = u;
-        d.vs[kind] = v;
-        d.Ks[kind] = max(d.Ks[kind], int(kk));
+        dst = max(dst, int(kk));
     };
-    if (o.cls == 1) cap(0, 1, 0, rhs_ram(F, g, 1, c.bcio));
-    else if (o.cls == 2) {
-        if (fl & HALDA_DEV_METAL_AVAIL) cap(1, 1, 0, rhs_ram(F, g, 2, c.bcio));
-    } else cap(2, 1, -1, rhs_ram(F, g, 3, c.bcio));
-    if (fl & HALDA_DEV_CUDA_OK) cap(3, 0, 1, rhs_cuda(F, g));
-    if (fl & HALDA_DEV_METAL_OK) cap(3, 0, 1, rhs_metal(Mo, F, g));
-    o.bad = bad;
-    return o;
-}
-
-__device__ inline void field_bounds(FieldDev &f, int W) {
-    f.d.whi = W;
-    f.d.nhi = f.gpu ? W : 0;
-    f.d.shi[0] = f.cls == 1 ? W : 0;
-    f.d.shi[1] = f.cls == 2 ? W : 0;
-    f.d.shi[2] = f.cls == 3 ? W : 0;
-    f.d.shi[3] = f.gpu ? W : 0;
+    if (r.cls == 1 || r.cls == 3 || (fl & HALDA_DEV_METAL_AVAIL)) K(rhs_ram(F, g, r.cls, c.bcio), r.Kset);
+    if (fl & HALDA_DEV_CUDA_OK) K(rhs_cuda(F, g), r.Kvram);
+    if (fl & HALDA_DEV_METAL_OK) K(rhs_metal(Mo, F, g), r.Kvram);
+    return r;
 }
 
 // Device records of a fleet straight from its table (the sweep's table path).
@@ -2506,11 +2527,38 @@ struct FieldSrc {
     int64_t d0;
     int W;
     __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
-        FieldDev f = field_dev(*Mo, *F, d0 + i);
-        field_bounds(f, W);
-        d = f.d;
+        int bad = 0;
+        FieldRec r = field_rec(*Mo, *F, d0 + i, bad);
+        r.W = W;
+        d = r.dev();
     }
 };
+
+// Objective constants of a fleet for the sweep's own obj_value (a fixed tree order: wave
+// reductions): sum t_comm, sum xi, kappa with the head's terms (dense_common.py:211-230).
+__device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
+                                          double &tsum, double &xsum, double &kappa) {
+    double t = 0.0, x = 0.0, tail = 0.0;
+    int hi = 0x7fffffff;
+    for (int i = lane; i < M; i += 64) {
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        t += F.t_comm[g];
+        x += (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
+        if (F.os_class[g] != 2) tail += double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        if (fl & HALDA_DEV_HEAD) hi = min(hi, i);
+    }
+    tsum = wave_sum_f64(t);
+    xsum = wave_sum_f64(x);
+    tail = wave_sum_f64(tail);
+    hi = wave_imin(hi);
+    const int64_t h = d0 + (hi == 0x7fffffff ? 0 : hi);
+    double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
+    total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
+    total += Mo.b_in / (Mo.V * F.s_disk[h]);
+    total += Mo.b_out / F.s_disk[h];
+    kappa = total + tail;
+}
 
 struct SweepArgs {
     halda_model Mo;
@@ -2552,15 +2600,18 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
     const int64_t d0 = F.dev_off[f];
     const int M = int(F.dev_off[f + 1] - d0);
     const bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
-    FieldDev me = {};
+    FieldRec me = {};
     int bad = 0;
-    if (regs && lane < M) me = field_dev(Mo, F, d0 + lane);
-    if (regs) bad = lane < M ? me.bad : 0;
-    else
-        for (int i = lane; i < M; i += 64) bad |= field_dev(Mo, F, d0 + i).bad;
+    if (regs && lane < M) me = field_rec(Mo, F, d0 + lane, bad);
+    if (!regs)
+        for (int i = lane; i < M; i += 64) {
+            int b1 = 0;
+            field_rec(Mo, F, d0 + i, b1);
+            bad |= b1;
+        }
     bad = wave_or(bad);
     double tsum = 0.0, xsum = 0.0, kappa = 0.0;
-    if (M > 0) fleet_offsets(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    if (M > 0) fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
     double best = kInf;
     int best_k = 0;
     for (int j = 0; j < A.n_k; ++j) {
@@ -2577,20 +2628,19 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
         else if (bad) st = HALDA_STATUS_UNSUPPORTED;
         else {
             int rc = K1_FALLBACK, e = 0, rounds = 0;
-            if (k == 1 && regs) {
-                field_bounds(me, W);
-                rc = k1_alloc(me.d, M, W - M, lane, e, rounds);
-            }
+            me.W = W;
+            if (k == 1 && regs) rc = k1_alloc(me, M, W - M, lane, e, rounds);
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
             } else if (rc == K1_OK) {
                 double g = 0.0, H = 0.0, z = 0.0;
                 int n = 0, sl[4] = {0, 0, 0, 0};
                 const int wl = 1 + e;
+                const Dev md = me.dev();
                 if (lane < M) {
                     double P, Q;
-                    split_full(me.d, wl, g, n, sl);
-                    dev_cycle(me.d, wl, n, sl, P, Q);
+                    split_full(md, wl, g, n, sl);
+                    dev_cycle(md, wl, n, sl, P, Q);
                     z = Q > P ? 0.5 * (Q - P) : 0.0;
                     H = Q >= P ? 0.5 * (P + Q) : P;
                 }
@@ -2602,7 +2652,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 st = HALDA_STATUS_OPTIMAL;
                 improved = obj < best;
                 if (lane < M) {
-                    put_xc(A, inst, M, lane, wl, n, sl, z, me.d);
+                    put_xc(A, inst, M, lane, wl, n, sl, z, md);
                     if (improved) {
                         A.out.w[d0 + lane] = wl;
                         A.out.n[d0 + lane] = n;
