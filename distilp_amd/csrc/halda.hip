@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "halda.h"
@@ -67,7 +68,15 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
     do {                                                                                                \
         if (lane == 0 && inst < kStampInst) g_halda_stamps[inst * kStamps + (slot)] = (v);              \
     } while (0)
+// fused sweep: per-fleet stamps (slot 0..6 shader clock, 7/8 constant-rate clock at start / end)
+#define HALDA_SSTAMP(slot, v)                                                                           \
+    do {                                                                                                \
+        if (lane == 0 && f < kStampInst) g_halda_stamps[int64_t(f) * kStamps + (slot)] = (v);           \
+    } while (0)
 #else
+#define HALDA_SSTAMP(slot, v) \
+    do {                      \
+    } while (0)
 #define HALDA_WSTAMP(slot, v) \
     do {                      \
     } while (0)
@@ -2129,42 +2138,71 @@ struct DevCoef {
     double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
 };
 
-__device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+// One device's table entry in registers: every field loaded unconditionally (one memory round
+// trip for all of them), the coefficients computed from the registers.
+struct DevFields {
+    double scpu, sgpu, Tc, Tg, tkc, tkg, r2v, v2r, tcomm, sdisk;
+    int64_t ram, ccpu, cgpu, cuda, metal, swap;
+    int cls, flags;
+};
+
+__device__ inline DevFields load_fields(const halda_fleets &F, int64_t g) {
+    DevFields f;
+    f.scpu = F.scpu_b1[g]; f.sgpu = F.sgpu_b1[g]; f.Tc = F.T_cpu[g]; f.Tg = F.T_gpu[g];
+    f.tkc = F.t_kvcpy_cpu[g]; f.tkg = F.t_kvcpy_gpu[g]; f.r2v = F.t_ram2vram[g]; f.v2r = F.t_vram2ram[g];
+    f.tcomm = F.t_comm[g]; f.sdisk = F.s_disk[g];
+    f.ram = F.d_avail_ram[g]; f.ccpu = F.c_cpu[g]; f.cgpu = F.c_gpu[g]; f.cuda = F.d_avail_cuda[g];
+    f.metal = F.d_avail_metal[g]; f.swap = F.swap[g];
+    f.cls = F.os_class[g];
+    f.flags = F.flags[g];
+    return f;
+}
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) {
     DevCoef o;
     const double bp = Mo.b_prime;
-    const uint8_t fl = F.flags[g];
-    const int cls = F.os_class[g];
-    const double Tc = F.T_cpu[g], tkc = F.t_kvcpy_cpu[g], tkg = F.t_kvcpy_gpu[g];
-    const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu_b1[g]);
+    const int fl = F.flags;
+    const int cls = F.cls;
+    const double Tc = F.Tc, tkc = F.tkc, tkg = F.tkg;
+    const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu);
     const bool hb = fl & HALDA_DEV_GPU;
-    const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu_b1[g]) : 0.0;
-    const double tg = hb ? F.T_gpu[g] : 1.0;
+    const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu) : 0.0;
+    const double tg = hb ? F.Tg : 1.0;
     o.alpha = (cpu + tkc) + (bp / Tc);
     const double beta = hb ? ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc) : 0.0;
     o.b = cls == 1 ? 0.0 : beta;
-    o.xi = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
+    o.xi = (F.r2v + F.v2r) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
     const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-    o.bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.c_cpu[g]);
-    const double sd = fmax(1.0, F.s_disk[g]);
+    o.bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.ccpu);
+    const double sd = fmax(1.0, F.sdisk);
     o.p_bp = bp / sd;
     o.p_b = Mo.b_layer / sd;
     o.p_v = cls == 2 ? o.p_b : o.p_bp;
-    o.cst = o.xi + F.t_comm[g];
+    o.cst = o.xi + F.tcomm;
     return o;
 }
 
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    return dev_coef(Mo, load_fields(F, g));
+}
+
 // Right-hand sides of the capacity rows (halda_p_solver.py:227-277).
+__device__ inline double rhs_ram(const DevFields &F, int set, double bcio) {
+    if (set == 1) return double(F.ram) - bcio;
+    if (set == 2) return double(F.metal) - bcio - double(F.cgpu);
+    return double(F.ram + F.swap) - bcio;
+}
+__device__ inline double rhs_cuda(const DevFields &F) { return double(F.cuda) - double(F.cgpu); }
+__device__ inline double rhs_metal(const halda_model &Mo, const DevFields &F) {
+    const double head = (F.flags & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+    return double(F.metal) - double(F.cgpu) - Mo.b_out * head;
+}
 __device__ inline double rhs_ram(const halda_fleets &F, int64_t g, int set, double bcio) {
-    if (set == 1) return double(F.d_avail_ram[g]) - bcio;
-    if (set == 2) return double(F.d_avail_metal[g]) - bcio - double(F.c_gpu[g]);
-    return double(F.d_avail_ram[g] + F.swap[g]) - bcio;
+    return rhs_ram(load_fields(F, g), set, bcio);
 }
-__device__ inline double rhs_cuda(const halda_fleets &F, int64_t g) {
-    return double(F.d_avail_cuda[g]) - double(F.c_gpu[g]);
-}
+__device__ inline double rhs_cuda(const halda_fleets &F, int64_t g) { return rhs_cuda(load_fields(F, g)); }
 __device__ inline double rhs_metal(const halda_model &Mo, const halda_fleets &F, int64_t g) {
-    const double head = (F.flags[g] & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-    return double(F.d_avail_metal[g]) - double(F.c_gpu[g]) - Mo.b_out * head;
+    return rhs_metal(Mo, load_fields(F, g));
 }
 
 // Objective constants of one fleet (lane-parallel loads, the reference's sequential sums over
@@ -2489,13 +2527,13 @@ struct FieldRec {
     }
 };
 
-__device__ inline FieldRec field_rec(const halda_model &Mo, const halda_fleets &F, int64_t g, int &bad) {
+__device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, int &bad) {
     FieldRec r;
-    const DevCoef c = dev_coef(Mo, F, g);
+    const DevCoef c = dev_coef(Mo, F);
     const double bp = Mo.b_prime;
-    const uint8_t fl = F.flags[g];
+    const int fl = F.flags;
     r.alpha = c.alpha; r.b = c.b; r.p_bp = c.p_bp; r.p_b = c.p_b; r.cst = c.cst;
-    r.cls = F.os_class[g];
+    r.cls = F.cls;
     r.gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1 : 0;
     r.W = 0;
     r.Kset = r.Kvram = kNoRow;
@@ -2514,9 +2552,9 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const halda_fleets &
         }
         dst = max(dst, int(kk));
     };
-    if (r.cls == 1 || r.cls == 3 || (fl & HALDA_DEV_METAL_AVAIL)) K(rhs_ram(F, g, r.cls, c.bcio), r.Kset);
-    if (fl & HALDA_DEV_CUDA_OK) K(rhs_cuda(F, g), r.Kvram);
-    if (fl & HALDA_DEV_METAL_OK) K(rhs_metal(Mo, F, g), r.Kvram);
+    if (r.cls == 1 || r.cls == 3 || (fl & HALDA_DEV_METAL_AVAIL)) K(rhs_ram(F, r.cls, c.bcio), r.Kset);
+    if (fl & HALDA_DEV_CUDA_OK) K(rhs_cuda(F), r.Kvram);
+    if (fl & HALDA_DEV_METAL_OK) K(rhs_metal(Mo, F), r.Kvram);
     return r;
 }
 
@@ -2528,36 +2566,56 @@ struct FieldSrc {
     int W;
     __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
         int bad = 0;
-        FieldRec r = field_rec(*Mo, *F, d0 + i, bad);
+        FieldRec r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
         r.W = W;
         d = r.dev();
     }
 };
 
 // Objective constants of a fleet for the sweep's own obj_value (a fixed tree order: wave
-// reductions): sum t_comm, sum xi, kappa with the head's terms (dense_common.py:211-230).
+// reductions): sum t_comm, sum xi, kappa with the head's terms (dense_common.py:211-230). For
+// M <= 64 lane i passes device i's fields (in registers) and the head's come by readlane.
+__device__ inline double tail_term(const DevFields &f) {
+    return f.cls != 2 ? double(f.ccpu - f.ram - f.swap) / f.sdisk : 0.0;
+}
+__device__ inline double xi_term(const DevFields &f) { return (f.r2v + f.v2r) * ((f.flags & HALDA_DEV_UMA) ? 0.0 : 1.0); }
+
+__device__ inline double kappa_head(const halda_model &Mo, int flags, double scpu, double Tc, double sdisk) {
+    double total = f_over_s(Mo.has_f_out && (flags & HALDA_DEV_CPU_RATE), Mo.f_out_b1, scpu);
+    total += (Mo.b_in / Mo.V + Mo.b_out) / Tc;
+    total += Mo.b_in / (Mo.V * sdisk);
+    total += Mo.b_out / sdisk;
+    return total;
+}
+
+__device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, int lane, double &tsum,
+                                          double &xsum, double &kappa) {
+    const bool act = lane < M;
+    tsum = wave_sum_f64(act ? mf.tcomm : 0.0);
+    xsum = wave_sum_f64(act ? xi_term(mf) : 0.0);
+    const double tail = wave_sum_f64(act ? tail_term(mf) : 0.0);
+    int hi = lowest_lane(act && (mf.flags & HALDA_DEV_HEAD));
+    if (hi > 63) hi = 0;
+    kappa = kappa_head(Mo, bcast(mf.flags, hi), bcast(mf.scpu, hi), bcast(mf.Tc, hi), bcast(mf.sdisk, hi)) + tail;
+}
+
 __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
                                           double &tsum, double &xsum, double &kappa) {
     double t = 0.0, x = 0.0, tail = 0.0;
     int hi = 0x7fffffff;
     for (int i = lane; i < M; i += 64) {
-        const int64_t g = d0 + i;
-        const uint8_t fl = F.flags[g];
-        t += F.t_comm[g];
-        x += (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
-        if (F.os_class[g] != 2) tail += double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
-        if (fl & HALDA_DEV_HEAD) hi = min(hi, i);
+        const DevFields f = load_fields(F, d0 + i);
+        t += f.tcomm;
+        x += xi_term(f);
+        tail += tail_term(f);
+        if (f.flags & HALDA_DEV_HEAD) hi = min(hi, i);
     }
     tsum = wave_sum_f64(t);
     xsum = wave_sum_f64(x);
     tail = wave_sum_f64(tail);
     hi = wave_imin(hi);
     const int64_t h = d0 + (hi == 0x7fffffff ? 0 : hi);
-    double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
-    total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
-    total += Mo.b_in / (Mo.V * F.s_disk[h]);
-    total += Mo.b_out / F.s_disk[h];
-    kappa = total + tail;
+    kappa = kappa_head(Mo, F.flags[h], F.scpu_b1[h], F.T_cpu[h], F.s_disk[h]) + tail;
 }
 
 struct SweepArgs {
@@ -2593,43 +2651,87 @@ __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, in
     }
 }
 
+#ifndef HALDA_SWEEP_TABLE_K1
+#define HALDA_SWEEP_TABLE_K1 1  // table launches also run the k = 1 register greedy (else k = 1 via tables)
+#endif
+
 template <bool kTables, bool kGlobal>
 __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lane) {
     const halda_model &Mo = A.Mo;
     const halda_fleets &F = A.F;
+    HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
     const int64_t d0 = F.dev_off[f];
     const int M = int(F.dev_off[f + 1] - d0);
     const bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
     FieldRec me = {};
     int bad = 0;
-    if (regs && lane < M) me = field_rec(Mo, F, d0 + lane, bad);
-    if (!regs)
+    double tsum = 0.0, xsum = 0.0, kappa = 0.0;
+    if (regs) {
+        // every field of this lane's device in one round trip (lanes past M read device 0)
+        const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        me = field_rec(Mo, mf, bad);
+        bad = lane < M ? bad : 0;
+        if (M > 0) fleet_offsets_regs(Mo, mf, M, lane, tsum, xsum, kappa);
+    } else {
         for (int i = lane; i < M; i += 64) {
             int b1 = 0;
-            field_rec(Mo, F, d0 + i, b1);
+            field_rec(Mo, load_fields(F, d0 + i), b1);
             bad |= b1;
         }
+        fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    }
     bad = wave_or(bad);
-    double tsum = 0.0, xsum = 0.0, kappa = 0.0;
-    if (M > 0) fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
     double best = kInf;
     int best_k = 0;
-    for (int j = 0; j < A.n_k; ++j) {
-        const int k = A.ks[j];
-        const int W = Mo.L / k;
+    // lane j: k_j and W_j = L / k_j; the k's settled without a solve (the screen's verdicts: W >= 1e6
+    // unsupported, M > W bound-infeasible, rows decode rejects) are written lane-parallel, and the
+    // loop below visits only the others, in ascending k
+    constexpr int kOpen = 1000;
+    const bool kl = lane < A.n_k;
+    const int kj = A.ks[kl ? lane : 0];
+    const int Wj = kl ? Mo.L / kj : 0;
+    int stj = kOpen;
+    if (!(Wj < 1000000)) stj = HALDA_STATUS_UNSUPPORTED;
+    else if (M > Wj) stj = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
+    else if (M > 0 && bad) stj = HALDA_STATUS_UNSUPPORTED;
+    if (kl && stj != kOpen) {
+        const int64_t inst = int64_t(f) * A.n_k + lane;
+        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
+        if (A.out.status) A.out.status[inst] = stj;
+    }
+    if (A.out.x || A.out.c) {  // x / c of a settled instance are zero
+        uint64_t settled = __ballot(kl && stj != kOpen);
+        const int N = 7 * M + 1;
+        while (settled) {
+            const int j = __builtin_ctzll(settled);
+            settled &= settled - 1;
+            const int64_t inst = int64_t(f) * A.n_k + j;
+            for (int cc = lane; cc < N; cc += 64) {
+                if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
+                if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
+            }
+        }
+    }
+    uint64_t todo = __ballot(kl && stj == kOpen);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int k = bcast(kj, j);
+        const int W = bcast(Wj, j);
         const int64_t inst = int64_t(f) * A.n_k + j;
         const double kc = double(k - 1);
         int st;
         double obj = kInf;
         bool improved = false;
-        if (!(W < 1000000)) st = HALDA_STATUS_UNSUPPORTED;  // the screen's W < 1e6
-        else if (M > W) st = HALDA_STATUS_INFEASIBLE;      // sum lb(w) = M > W (HiGHS presolve)
-        else if (M == 0) st = W > 0 ? HALDA_STATUS_INFEASIBLE : HALDA_STATUS_OPTIMAL;  // x = [C = 0]
-        else if (bad) st = HALDA_STATUS_UNSUPPORTED;
+        if (M == 0) st = W > 0 ? HALDA_STATUS_INFEASIBLE : HALDA_STATUS_OPTIMAL;  // x = [C = 0]
         else {
             int rc = K1_FALLBACK, e = 0, rounds = 0;
             me.W = W;
-            if (k == 1 && regs) rc = k1_alloc(me, M, W - M, lane, e, rounds);
+            if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
+            if (k == 1 && regs && (!kTables || HALDA_SWEEP_TABLE_K1)) rc = k1_alloc(me, M, W - M, lane, e, rounds);
+            if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
             } else if (rc == K1_OK) {
@@ -2662,6 +2764,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                     if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
                     if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
                 }
+                HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
             } else if constexpr (!kTables) {
                 // k > 1, a wide fleet or a fast-path fallback: the table launch redoes this fleet
                 if (lane == 0) {
@@ -2749,6 +2852,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
             if (A.out.status) A.out.status[inst] = st;
         }
     }
+    HALDA_SSTAMP(5, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
         A.out.best_k[f] = best_k;
         A.out.obj_value[f] = best;
@@ -2759,6 +2863,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
             A.out.w[d0 + i] = 0;
             A.out.n[d0 + i] = 0;
         }
+    HALDA_SSTAMP(6, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(8, __builtin_amdgcn_s_memrealtime());
 }
 
 template <bool kTables, bool kGlobal>
@@ -3167,10 +3273,11 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned(nf)), dim3(64), 0, s, A);
         HIP_TRY(hipGetLastError());
         A.want = 1;  // the fleets flagged above, gated on the hand-back flag
-        if (fits) {
+        if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
             int per_cu = 0;
             HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-            const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
+            const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tables_first ? int64_t(c->cus) * per_cu
+                                                                                   : int64_t(c->cus), nf)));
             hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
         } else {
             A.gstride = (slice + 255) & ~int64_t(255);
@@ -3594,6 +3701,89 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     HIP_TRY(down(out_h->x, o_x, 8 * xs));
     HIP_TRY(down(out_h->c, o_c, 8 * xs));
     HIP_TRY(hipStreamSynchronize(s));
+    return HALDA_OK;
+}
+
+// ---------------------------------------------------------------- several GPUs, one process
+// The fleets of one call are independent: a multi-device context deals them out in contiguous
+// blocks, one host thread per device runs halda_solve_fleets_host on its block, and the results
+// land in the caller's arrays at the block's offsets. No collective is needed (the argmin over k is
+// per fleet, on the device that solved it); multi-process / multi-node callers use one halda_init
+// context per rank and torch.distributed / RCCL around it (distilp_amd/distributed.py).
+struct MultiCtx {
+    std::vector<void *> ctxs;
+};
+
+int halda_init_multi(int n_dev, const int *ordinals, void **mctx) {
+    if (!mctx || n_dev < 1 || n_dev > 64 || !ordinals) return fail(HALDA_E_ARG, "halda_init_multi: bad arguments");
+    MultiCtx *m = new MultiCtx();
+    for (int i = 0; i < n_dev; ++i) {
+        void *c = nullptr;
+        const int rc = halda_init(ordinals[i], &c);
+        if (rc != HALDA_OK) {
+            for (void *o : m->ctxs) halda_free(o);
+            delete m;
+            return rc;
+        }
+        m->ctxs.push_back(c);
+    }
+    *mctx = m;
+    return HALDA_OK;
+}
+
+void halda_free_multi(void *mctx) {
+    MultiCtx *m = static_cast<MultiCtx *>(mctx);
+    if (!m) return;
+    for (void *c : m->ctxs) halda_free(c);
+    delete m;
+}
+
+int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_fleets *fh, const int32_t *ks,
+                             int32_t n_k, halda_fleet_result *out_h) {
+    MultiCtx *m = static_cast<MultiCtx *>(mctx);
+    if (!m || !model || !fh || !ks || !out_h || !fh->dev_off) return fail(HALDA_E_ARG, "NULL argument");
+    const int nd = int(m->ctxs.size()), nf = fh->n_fleets;
+    if (nf <= 0) return HALDA_OK;
+    const int64_t xs = 7 * int64_t(std::max(fh->max_devices, 1)) + 1;
+    std::vector<std::vector<int64_t>> offs(nd);
+    std::vector<int> rcs(nd, HALDA_OK);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    for (int r = 0; r < nd; ++r) {
+        const int base = nf / nd, extra = nf % nd;
+        const int lo = r * base + std::min(r, extra), hi = lo + base + (r < extra ? 1 : 0);
+        if (hi <= lo) continue;
+        const int64_t d0 = fh->dev_off[lo];
+        offs[r].resize(size_t(hi - lo + 1));
+        for (int f = lo; f <= hi; ++f) offs[r][size_t(f - lo)] = fh->dev_off[f] - d0;
+        th.emplace_back([&, r, lo, hi, d0]() {
+            halda_fleets sub = *fh;  // min / max devices stay the call's (valid bounds for the block)
+            sub.n_fleets = hi - lo;
+            sub.dev_off = offs[r].data();
+            sub.os_class = fh->os_class + d0;
+            sub.flags = fh->flags + d0;
+            sub.scpu_b1 = fh->scpu_b1 + d0; sub.sgpu_b1 = fh->sgpu_b1 + d0; sub.T_cpu = fh->T_cpu + d0;
+            sub.T_gpu = fh->T_gpu + d0; sub.t_kvcpy_cpu = fh->t_kvcpy_cpu + d0; sub.t_kvcpy_gpu = fh->t_kvcpy_gpu + d0;
+            sub.t_ram2vram = fh->t_ram2vram + d0; sub.t_vram2ram = fh->t_vram2ram + d0; sub.t_comm = fh->t_comm + d0;
+            sub.s_disk = fh->s_disk + d0; sub.d_avail_ram = fh->d_avail_ram + d0; sub.c_cpu = fh->c_cpu + d0;
+            sub.c_gpu = fh->c_gpu + d0; sub.d_avail_cuda = fh->d_avail_cuda + d0;
+            sub.d_avail_metal = fh->d_avail_metal + d0; sub.swap = fh->swap + d0;
+            halda_fleet_result o = *out_h;
+            o.best_k = out_h->best_k + lo;
+            o.obj_value = out_h->obj_value + lo;
+            o.w = out_h->w + d0;
+            o.n = out_h->n + d0;
+            o.obj_by_k = out_h->obj_by_k ? out_h->obj_by_k + int64_t(lo) * n_k : nullptr;
+            o.status = out_h->status ? out_h->status + int64_t(lo) * n_k : nullptr;
+            o.x = out_h->x ? out_h->x + int64_t(lo) * n_k * xs : nullptr;
+            o.c = out_h->c ? out_h->c + int64_t(lo) * n_k * xs : nullptr;
+            rcs[r] = halda_solve_fleets_host(m->ctxs[size_t(r)], model, &sub, ks, n_k, &o);
+            if (rcs[r] != HALDA_OK) errs[r] = g_err;
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int r = 0; r < nd; ++r)
+        if (rcs[r] != HALDA_OK) return fail(rcs[r], "device " + std::to_string(r) + ": " + errs[r]);
     return HALDA_OK;
 }
 

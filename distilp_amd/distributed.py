@@ -3,15 +3,17 @@
 Two modes:
 
 * throughput (`halda_solve_batch_distributed`, configs C3/C5): fleets are
-  independent, so each rank solves a contiguous shard of them on its own GPU —
-  no collective on the data path; results are gathered once at the end.
+  independent, so each rank solves a contiguous shard of them on its own GPU as
+  one halda_solve_fleets k-sweep (device-field table, no host lowering) — no
+  collective on the data path; results are gathered once at the end.
 * latency (`halda_solve_distributed`, one fleet, config C2 at 8 GPUs): the
   k-candidates are dealt round-robin over the ranks, each rank solves its k's
   exactly, then ONE all-reduce(min) of the objective (8 B) and one of the
   winning k (ties -> smallest k, the reference's strict "<" over ascending k,
   halda_p_solver.py:407) pick the answer; its owner broadcasts (w, n).
 
-The per-rank engine is libhalda on the rank's GPU. `_solve` is an injection
+The per-rank engine is libhalda on the rank's GPU (tests/test_gpu_distributed.py
+runs both modes with it: two gloo ranks on one GPU). `_solve` is an injection
 point for tests of the orchestration on CPU (gloo); it is never an engine
 fallback.
 """
@@ -35,17 +37,16 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def _default_solve(device: int) -> Callable:
-    from .solver.batch import assemble
-    from .solver.halda import _results_for
-    from .solver._libhalda import get_context
-    from .solver.lower import lower_fleet
+    """Per-k results of each fleet on this rank's GPU: one halda_solve_fleets k-sweep per fleet with
+    obj_value formed on the host exactly as the reference forms it (solver.halda._sweep_on_gpu)."""
+    from .solver.coefficients import assign_sets as _sets
+    from .solver.halda import _sweep_on_gpu
+    from .solver.lower import kv_bits_to_factor
 
     def solve(fleets: Sequence[List[DeviceProfile]], model: ModelProfile, ks: Sequence[int], kv_bits: str,
               mip_gap: float) -> List[PerK]:
-        lowered = [lower_fleet(devs, model, kv_bits) for devs in fleets]
-        batch, refs = assemble(lowered, [list(ks)] * len(lowered), mip_gap)
-        res = get_context(device).solve(batch)
-        return _results_for(lowered, refs, res)
+        kv = kv_bits_to_factor(kv_bits)
+        return [_sweep_on_gpu(list(devs), model, _sets(list(devs)), list(ks), kv, device, False) for devs in fleets]
 
     return solve
 
@@ -125,18 +126,25 @@ def halda_solve_batch_distributed(fleets: Sequence[List[DeviceProfile]], model: 
         L = model.L
         Ks = sorted({d for d in range(1, L) if L % d == 0})
     lo, hi = shard_bounds(len(fleets), rank, world)
-    solve = _solve or _default_solve(torch.cuda.current_device() if device is None else device)
-    local = solve(list(fleets[lo:hi]), model, Ks, kv_bits, mip_gap) if hi > lo else []
     results: List[Optional[HALDAResult]] = []
-    for devs, per_k in zip(fleets[lo:hi], local):
-        best: Optional[ILPResult] = None
-        for _, r in per_k:
-            if r is not None and (best is None or r.obj_value < best.obj_value):
-                best = r
-        sets = assign_sets(devs)
-        results.append(None if best is None else HALDAResult(w=list(best.w), n=list(best.n), k=best.k,
-                                                             obj_value=best.obj_value,
-                                                             sets={s: list(v) for s, v in sets.items()}))
+    if _solve is None and hi > lo:
+        # the rank's shard as ONE GPU k-sweep (halda_solve_fleets: fused sweep from the device-field table)
+        from .solver.fleets import halda_solve_fleets
+
+        dev = torch.cuda.current_device() if device is None else device
+        results = halda_solve_fleets(list(fleets[lo:hi]), model, k_candidates=Ks, mip_gap=mip_gap, kv_bits=kv_bits,
+                                     device=dev) if Ks else [None] * (hi - lo)
+    elif hi > lo:
+        local = _solve(list(fleets[lo:hi]), model, Ks, kv_bits, mip_gap)
+        for devs, per_k in zip(fleets[lo:hi], local):
+            best: Optional[ILPResult] = None
+            for _, r in per_k:
+                if r is not None and (best is None or r.obj_value < best.obj_value):
+                    best = r
+            sets = assign_sets(devs)
+            results.append(None if best is None else HALDAResult(w=list(best.w), n=list(best.n), k=best.k,
+                                                                 obj_value=best.obj_value,
+                                                                 sets={s: list(v) for s, v in sets.items()}))
     if not gather:
         return lo, results
     everything = [None] * world

@@ -71,6 +71,14 @@ def _bind(lib):
     lib.halda_solve_fleets_host.restype = ctypes.c_int
     lib.halda_last_lowered.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC), ctypes.POINTER(HaldaResultC)]
     lib.halda_last_lowered.restype = ctypes.c_int
+    lib.halda_init_multi.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+    lib.halda_init_multi.restype = ctypes.c_int
+    lib.halda_solve_fleets_multi.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaModelC),
+                                             ctypes.POINTER(HaldaFleetsC), ctypes.c_void_p, ctypes.c_int32,
+                                             ctypes.POINTER(HaldaFleetResultC)]
+    lib.halda_solve_fleets_multi.restype = ctypes.c_int
+    lib.halda_free_multi.argtypes = [ctypes.c_void_p]
+    lib.halda_free_multi.restype = None
     lib._fleets_bound = True
     return lib
 
@@ -139,17 +147,19 @@ class FleetTable:
         upd.update({f: np.floor(getattr(self, f) * lu()).astype(np.int64) for f in I64_FIELDS})
         return replace(self, **upd)
 
-    def check(self) -> None:
-        """The reference's ZeroDivisionErrors (alpha: bp / T_cpu; kappa: head and M1/M3 s_disk)."""
+    def check(self, heads: Optional[np.ndarray] = None) -> None:
+        """The reference's ZeroDivisionErrors (alpha: bp / T_cpu; kappa: head and M1/M3 s_disk).
+        heads: global index of each fleet's kappa head (first is_head device, else its first)."""
         if np.any(self.T_cpu == 0.0):
             raise ZeroDivisionError("float division by zero")
-        head = self.flags & DEV_HEAD
-        for f in range(self.n_fleets):
-            a, b = self.dev_off[f], self.dev_off[f + 1]
-            hs = np.nonzero(head[a:b])[0]
-            h = a + (int(hs[0]) if len(hs) else 0)
-            if self.s_disk[h] == 0.0 or np.any((self.os_class[a:b] != 2) & (self.s_disk[a:b] == 0.0)):
-                raise ZeroDivisionError("float division by zero")
+        if heads is None:
+            heads = np.empty(self.n_fleets, np.int64)
+            for f in range(self.n_fleets):
+                a, b = self.dev_off[f], self.dev_off[f + 1]
+                hs = np.nonzero(self.flags[a:b] & DEV_HEAD)[0]
+                heads[f] = a + (int(hs[0]) if len(hs) else 0)
+        if np.any(self.s_disk[heads] == 0.0) or np.any((self.os_class != 2) & (self.s_disk == 0.0)):
+            raise ZeroDivisionError("float division by zero")
 
 
 def _rate(table, q, f_has_b1: bool, raise_on_missing: bool) -> tuple:
@@ -167,57 +177,63 @@ def _rate(table, q, f_has_b1: bool, raise_on_missing: bool) -> tuple:
 
 
 def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
-    """Pack fleets (lists of DeviceProfile) into a FleetTable."""
+    """Pack fleets (lists of DeviceProfile) into a FleetTable (one row tuple per device, then one
+    NumPy conversion per field group)."""
     Q = model.Q
     fq, fout = "b_1" in model.f_q, "b_1" in model.f_out
-    cls, flags, cols = [], [], {f: [] for f in F64_FIELDS + I64_FIELDS}
+    cls, flags, f64, i64, heads = [], [], [], [], []
     off = [0]
+    os_code = {"mac_no_metal": 1, "mac_metal": 2}
     for devs in fleets:
         if not devs:
             raise IndexError("list index out of range")  # the reference's kappa on an empty fleet
         head = next((i for i, d in enumerate(devs) if d.is_head), 0)  # kappa's head (dense_common.py:214-219)
+        heads.append(off[-1] + head)
         for i, d in enumerate(devs):
-            cls.append({"mac_no_metal": 1, "mac_metal": 2}.get(d.os_type, 3))
-            fl = (DEV_HEAD if d.is_head else 0) | (DEV_UMA if d.is_unified_mem else 0)
+            g = d.__dict__  # pydantic v2 keeps field values here: plain dict reads, no descriptor per field
+            os_type = g["os_type"]
+            cls.append(os_code.get(os_type, 3))
+            fl = (DEV_HEAD if g["is_head"] else 0) | (DEV_UMA if g["is_unified_mem"] else 0)
             # alpha reads scpu with f_q; kappa reads the head's scpu with f_out
-            ok, v = _rate(d.scpu, Q, fq, True)
-            if i == head:
-                _rate(d.scpu, Q, fout, True)
-            fl |= DEV_CPU_RATE if ok else 0
-            table, tg = gpu_flops_table(d), gpu_load_throughput(d)
+            sc = g["scpu"]
+            row = sc.get(Q) if sc else None
+            v = 0.0
+            if row is not None:
+                if "b_1" in row:
+                    v = float(row["b_1"])
+                    fl |= DEV_CPU_RATE
+                elif fq or (fout and i == head):
+                    raise ValueError(f"Batch size 1 (key 'b_1') not found in S_by_q[{Q}]")
+            has_metal, has_cuda = g["has_metal"], g["has_cuda"]
+            # _gpu_table / _pick_T_gpu (dense_common.py:78-97): Metal preferred, truthiness tests
+            table = g["sgpu_metal"] if has_metal and g["sgpu_metal"] else (
+                g["sgpu_cuda"] if has_cuda and g["sgpu_cuda"] else None)
+            tg = g["T_metal"] if has_metal and g["T_metal"] else (g["T_cuda"] if has_cuda and g["T_cuda"] else None)
             gv, tgv = 0.0, 1.0
             if table is not None and tg is not None:
                 fl |= DEV_GPU
                 gok, gv = _rate(table, Q, fq, True)
-                fl |= DEV_GPU_RATE if gok else 0
+                if gok:
+                    fl |= DEV_GPU_RATE
                 tgv = float(tg)
-            fl |= DEV_CUDA_OK if (d.has_cuda and d.d_avail_cuda is not None) else 0
-            fl |= DEV_METAL_OK if (d.has_metal and d.d_avail_metal is not None) else 0
-            fl |= DEV_METAL_AVAIL if d.d_avail_metal is not None else 0
+            dc, dm = g["d_avail_cuda"], g["d_avail_metal"]
+            if has_cuda and dc is not None:
+                fl |= DEV_CUDA_OK
+            if dm is not None:
+                fl |= DEV_METAL_AVAIL | (DEV_METAL_OK if has_metal else 0)
             flags.append(fl)
-            c = cols
-            c["scpu_b1"].append(v)
-            c["sgpu_b1"].append(gv)
-            c["T_cpu"].append(d.T_cpu)
-            c["T_gpu"].append(tgv)
-            c["t_kvcpy_cpu"].append(d.t_kvcpy_cpu)
-            c["t_kvcpy_gpu"].append(d.t_kvcpy_gpu)
-            c["t_ram2vram"].append(d.t_ram2vram)
-            c["t_vram2ram"].append(d.t_vram2ram)
-            c["t_comm"].append(d.t_comm)
-            c["s_disk"].append(d.s_disk)
-            c["d_avail_ram"].append(d.d_avail_ram)
-            c["c_cpu"].append(d.c_cpu)
-            c["c_gpu"].append(d.c_gpu)
-            c["d_avail_cuda"].append(d.d_avail_cuda or 0)
-            c["d_avail_metal"].append(d.d_avail_metal or 0)
-            c["swap"].append(min(d.d_bytes_can_swap, d.d_swap_avail) if d.os_type == "android" else 0)
+            f64.append((v, gv, g["T_cpu"], tgv, g["t_kvcpy_cpu"], g["t_kvcpy_gpu"], g["t_ram2vram"], g["t_vram2ram"],
+                        g["t_comm"], g["s_disk"]))
+            i64.append((g["d_avail_ram"], g["c_cpu"], g["c_gpu"], dc or 0, dm or 0,
+                        min(g["d_bytes_can_swap"], g["d_swap_avail"]) if os_type == "android" else 0))
         off.append(off[-1] + len(devs))
+    fa = np.array(f64, dtype=np.float64).reshape(-1, len(F64_FIELDS))
+    ia = np.array(i64, dtype=np.int64).reshape(-1, len(I64_FIELDS))
     t = FleetTable(dev_off=np.asarray(off, np.int64), os_class=np.asarray(cls, np.uint8),
                    flags=np.asarray(flags, np.uint8),
-                   **{f: np.asarray(cols[f], np.float64) for f in F64_FIELDS},
-                   **{f: np.asarray(cols[f], np.int64) for f in I64_FIELDS})
-    t.check()
+                   **{f: np.ascontiguousarray(fa[:, j]) for j, f in enumerate(F64_FIELDS)},
+                   **{f: np.ascontiguousarray(ia[:, j]) for j, f in enumerate(I64_FIELDS)})
+    t.check(np.asarray(heads, np.int64))
     return t
 
 
@@ -253,8 +269,38 @@ def _k_list(model: ModelProfile, k_candidates: Optional[Iterable[int]]) -> List[
     return sorted({d for d in range(1, L) if L % d == 0}) if L > 1 else []
 
 
+class MultiDeviceContext:
+    """libhalda multi-device context (halda_init_multi): one context per GPU ordinal of one process;
+    solve() deals a FleetTable's fleets out over them (halda_solve_fleets_multi)."""
+
+    def __init__(self, devices: Sequence[int]):
+        from ._libhalda import HaldaUnavailable, load_library
+
+        self.lib = _bind(load_library())
+        ords = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.halda_init_multi(len(devices), ords, ctypes.byref(self.ctx))
+        if rc != 0:
+            raise HaldaUnavailable(f"halda_init_multi({list(devices)}) failed ({rc}): {last_error(self.lib)}")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.halda_free_multi(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
+              want_x: bool = False) -> "FleetSolve":
+        return solve_table(table, model, ks, kv_factor, want_x=want_x, _multi=self)
+
+
 def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
-                device: int = 0, want_x: bool = False) -> FleetSolve:
+                device: int = 0, want_x: bool = False, _multi: Optional["MultiDeviceContext"] = None) -> FleetSolve:
     """halda_solve_fleets_host on a host FleetTable (synchronous). want_x: also x and the lowered c
     of every (fleet, k) (so the host can form obj_value exactly as the reference, with NumPy)."""
     ks = [int(k) for k in ks]
@@ -262,8 +308,8 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
         raise ValueError("no k-candidates")
     if ks[0] <= 0:
         raise ZeroDivisionError("integer division or modulo by zero")
-    ctx = get_context(device)
-    lib = _bind(ctx.lib)
+    ctx = get_context(device) if _multi is None else None
+    lib = _bind(ctx.lib) if _multi is None else _multi.lib
     arrs = {f: np.ascontiguousarray(getattr(table, f)) for f in ("dev_off", "os_class", "flags") + F64_FIELDS
             + I64_FIELDS}
     fs = _fleets_struct(table, lambda f: arrs[f].ctypes.data)
@@ -279,9 +325,13 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
                           out.x.ctypes.data if want_x else None, out.c.ctypes.data if want_x else None)
     karr = np.asarray(ks, np.int32)
     m = model_struct(model, kv_factor)
-    with ctx._lock:
-        rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
-                                         ctypes.byref(r))
+    if _multi is not None:
+        rc = lib.halda_solve_fleets_multi(_multi.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
+                                          ctypes.byref(r))
+    else:
+        with ctx._lock:
+            rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
+                                             ctypes.byref(r))
     if rc != 0:
         raise RuntimeError(f"halda_solve_fleets_host failed ({rc}): {last_error(lib)}")
     return out

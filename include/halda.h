@@ -212,6 +212,16 @@ int halda_last_fleet_ms(void *ctx, double *ms6);
 int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                             int32_t n_k, halda_fleet_result *out);
 
+/* Several GPUs from one process: a context per device (ordinals may repeat), and
+ * halda_solve_fleets_host over all of them -- the fleets are dealt out in contiguous blocks, one host
+ * thread per device, results written at each block's offsets. Fleets are independent, so no
+ * collective is involved; multi-process / multi-node callers use one halda_init context per rank
+ * (distilp_amd/distributed.py: torch.distributed / RCCL around it). */
+int halda_init_multi(int n_dev, const int *ordinals, void **mctx);
+int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                             int32_t n_k, halda_fleet_result *out);
+void halda_free_multi(void *mctx);
+
 /* The lowered batch of the last halda_solve_fleets call (device pointers into ctx
  * scratch, valid until the next call on ctx): for tests and diagnostics. An
  * instance with L / k < M (bound-infeasible) carries only its header, w bounds,

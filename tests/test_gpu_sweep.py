@@ -83,3 +83,25 @@ def test_fused_sweep_rejects_what_decode_rejects(llama_online_model):
     assert np.array_equal(fused.status, csr.status)
     W = [80 // k for k in ks]
     assert [int(s) for s in fused.status[0]] == [STATUS_UNSUPPORTED if w >= 6 else STATUS_INFEASIBLE for w in W]
+
+
+def test_multi_device_context_equals_single(llama_online_model):
+    """halda_init_multi / halda_solve_fleets_multi: fleets dealt over several contexts (here three on
+    GPU 0) give exactly the single-context answers, x and per-k results included."""
+    from distilp_amd.solver.fleets import MultiDeviceContext
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(9000 + s, M)]
+              for s, M in enumerate([3, 16, 64, 5, 70, 12, 2, 33, 8, 64, 1])]
+    table = fleet_table(fleets, llama_online_model)
+    one = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+    multi = MultiDeviceContext([0, 0, 0])
+    try:
+        many = multi.solve(table, llama_online_model, ks, 0.5, want_x=True)
+    finally:
+        multi.close()
+    for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status"):
+        assert np.array_equal(getattr(one, f), getattr(many, f)), f
+    for fi, devs in enumerate(fleets):  # x / c are defined on each fleet's 7 M + 1 columns
+        N = 7 * len(devs) + 1
+        assert np.array_equal(one.x[fi, :, :N], many.x[fi, :, :N]) and np.array_equal(one.c[fi, :, :N], many.c[fi, :, :N])
