@@ -1054,14 +1054,16 @@ struct CsrSrc {
 // Fleets of at most 32 devices spread each device's chain over P = 64 / M lanes
 // (each starts its stretch of e with a full split search): the least minimiser
 // n*(w) is the same either way, so G and H are too.
+// src.load runs on every lane (index clamped to a valid device) so that a source may shuffle
+// records between lanes.
 template <class Src>
 __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int lane) {
     if (I.M <= 32) {
         const int P = 64 / I.M, chunk = (I.R1 + P - 1) / P;
         const int i = lane / P, p = lane - i * P;
+        Dev d;
+        src.load(d, w, min(i, I.M - 1));
         if (i < I.M) {
-            Dev d;
-            src.load(d, w, i);
             int n = 0;
             bool have = false;
             const int e1 = min(I.R1, (p + 1) * chunk);
@@ -1069,12 +1071,15 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
         }
         return;
     }
-    for (int i = lane; i < I.M; i += 64) {
+    for (int i0 = 0; i0 < I.M; i0 += 64) {
+        const int i = i0 + lane;
         Dev d;
-        src.load(d, w, i);
-        int n = 0;
-        bool have = false;
-        for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
+        src.load(d, w, min(i, I.M - 1));
+        if (i < I.M) {
+            int n = 0;
+            bool have = false;
+            for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
+        }
     }
 }
 
@@ -2515,6 +2520,16 @@ struct FieldRec {
         d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
         return d;
     }
+    __device__ inline FieldRec shfl(int src) const {  // per-lane source (all lanes active)
+        FieldRec o;
+        o.alpha = shfl_f64(alpha, src); o.b = shfl_f64(b, src); o.p_bp = shfl_f64(p_bp, src);
+        o.p_b = shfl_f64(p_b, src); o.cst = shfl_f64(cst, src);
+        o.Kset = __shfl(Kset, src); o.Kvram = __shfl(Kvram, src);
+        const int cg = __shfl(cls | (gpu << 4), src);
+        o.cls = cg & 15; o.gpu = cg >> 4;
+        o.W = W;
+        return o;
+    }
     __device__ inline FieldRec bcast(int src) const {
         FieldRec o;
         o.alpha = ::bcast(alpha, src); o.b = ::bcast(b, src); o.p_bp = ::bcast(p_bp, src);
@@ -2559,14 +2574,23 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, 
 }
 
 // Device records of a fleet straight from its table (the sweep's table path).
+// Device records of a fleet for the sweep's table path: for M <= 64 lane i already holds device
+// i's record (me), which other lanes fetch by shuffle; wider fleets rebuild it from the table.
+// load() runs on every lane (uniform control flow: the shuffles read every lane's registers).
 struct FieldSrc {
     const halda_model *Mo;
     const halda_fleets *F;
+    const FieldRec *me;  // lane's own record (M <= 64), or nullptr
     int64_t d0;
     int W;
     __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
-        int bad = 0;
-        FieldRec r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
+        FieldRec r;
+        if (me) {
+            r = me->shfl(i);
+        } else {
+            int bad = 0;
+            r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
+        }
         r.W = W;
         d = r.dev();
     }
@@ -2781,7 +2805,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 I.iC = 7 * M;
                 I.R1 = W - M + 1;
                 I.RS = odd_stride(I.R1);
-                const FieldSrc src{&A.Mo, &A.F, d0, W};
+                const FieldSrc src{&A.Mo, &A.F, regs ? &me : nullptr, d0, W};
                 int64_t nodes = 0;
                 if (M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab)) {
                     st = HALDA_STATUS_TOO_LARGE;  // beyond the launch's slice (the host sizes it from the fleets)
@@ -2790,17 +2814,20 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 } else {
                     // solution: per device (w, n, least slacks, z), sum of costs, largest cycle time
                     double gs = 0.0, hmax = 0.0;
-                    for (int i = lane; i < M; i += 64) {
+                    for (int i0 = 0; i0 < M; i0 += 64) {
+                        const int i = i0 + lane;
                         Dev d;
-                        src.load(d, w, i);
-                        const int wl = 1 + w.st0[i];
-                        double g = 0.0, P, Q;
-                        int n = 0, sl[4] = {0, 0, 0, 0};
-                        split_full(d, wl, g, n, sl);
-                        dev_cycle(d, wl, n, sl, P, Q);
-                        gs += g;
-                        hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
-                        put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
+                        src.load(d, w, min(i, M - 1));
+                        if (i < M) {
+                            const int wl = 1 + w.st0[i];
+                            double g = 0.0, P, Q;
+                            int n = 0, sl[4] = {0, 0, 0, 0};
+                            split_full(d, wl, g, n, sl);
+                            dev_cycle(d, wl, n, sl, P, Q);
+                            gs += g;
+                            hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
+                            put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
+                        }
                     }
                     hmax = wave_max(hmax);
                     obj = wave_sum_f64(gs) + kc * hmax;
@@ -2810,15 +2837,18 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                     st = HALDA_STATUS_OPTIMAL;
                     improved = obj < best;
                     if (improved)
-                        for (int i = lane; i < M; i += 64) {
+                        for (int i0 = 0; i0 < M; i0 += 64) {
+                            const int i = i0 + lane;
                             Dev d;
-                            src.load(d, w, i);
-                            const int wl = 1 + w.st0[i];
-                            double g;
-                            int n = 0, sl[4];
-                            split_full(d, wl, g, n, sl);
-                            A.out.w[d0 + i] = wl;
-                            A.out.n[d0 + i] = n;
+                            src.load(d, w, min(i, M - 1));
+                            if (i < M) {
+                                const int wl = 1 + w.st0[i];
+                                double g;
+                                int n = 0, sl[4];
+                                split_full(d, wl, g, n, sl);
+                                A.out.w[d0 + i] = wl;
+                                A.out.n[d0 + i] = n;
+                            }
                         }
                     if (lane == 0) {
                         if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
