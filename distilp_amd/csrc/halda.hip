@@ -68,15 +68,26 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
     do {                                                                                                \
         if (lane == 0 && inst < kStampInst) g_halda_stamps[inst * kStamps + (slot)] = (v);              \
     } while (0)
-// fused sweep: per-fleet stamps (slot 0..6 shader clock, 7/8 constant-rate clock at start / end)
+// fused sweep: per-fleet stamps (slot 0..6 shader clock, 7/8 constant-rate clock at start / end);
+// with -DHALDA_STAMPS_DP per-instance stamps of the table path instead (HALDA_TSTAMP, slots 0, 6-8)
+#ifdef HALDA_STAMPS_DP
+#define HALDA_SSTAMP(slot, v) do {} while (0)
+#define HALDA_TSTAMP(slot)                                                                              \
+    do {                                                                                                \
+        if (lane == 0 && inst < kStampInst) g_halda_stamps[inst * kStamps + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
 #define HALDA_SSTAMP(slot, v)                                                                           \
     do {                                                                                                \
         if (lane == 0 && f < kStampInst) g_halda_stamps[int64_t(f) * kStamps + (slot)] = (v);           \
     } while (0)
+#define HALDA_TSTAMP(slot) do {} while (0)
+#endif
 #else
 #define HALDA_SSTAMP(slot, v) \
     do {                      \
     } while (0)
+#define HALDA_TSTAMP(slot) do {} while (0)
 #define HALDA_WSTAMP(slot, v) \
     do {                      \
     } while (0)
@@ -1173,16 +1184,21 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
         const int ljo = lj;
         S += swap ? d - lam : d;
         if (!swap) --need;
-        if (lane == li) {  // li takes the unit its new cap opens
-            cap = e + 1;
-            e = cap;
-            hn = cap < hi ? H[cap + 1] : kInf;
-            gn = cap < hi ? G[cap + 1] - G[cap] : kInf;
-            lt = G[e] - G[e - 1];
-        }
-        if (swap && lane == ljo) {  // ljo gives back its largest taken unit
-            --e;
-            lt = e > lo ? G[e] - G[e - 1] : -kInf;
+        // li takes the unit its new cap opens; ljo gives back its largest taken unit (li == ljo only
+        // through the convexity tolerance: then in that order). All LDS reads in one round trip.
+        const bool is_li = lane == li, is_lj = swap && lane == ljo;
+        if (is_li || is_lj) {
+            const int ncap = is_li ? e + 1 : cap;
+            const int ne = is_li ? (is_lj ? e : e + 1) : e - 1;
+            const int a = min(ncap + 1, hi), b = max(ne - 1, 0);
+            const double Gn1 = G[a], Gn0 = G[ncap], Hn1 = H[a], Ge = G[ne], Gm = G[b];
+            if (is_li) {
+                cap = ncap;
+                hn = cap < hi ? Hn1 : kInf;
+                gn = cap < hi ? Gn1 - Gn0 : kInf;
+            }
+            e = ne;
+            lt = is_lj ? (e > lo ? Ge - Gm : -kInf) : Ge - Gm;
         }
         if (need == 0) {
             lam = wave_max(lt);
@@ -1203,10 +1219,83 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     return true;
 }
 
+// k > 1 for fleets of at most 64 devices with convex leaves and nondecreasing cycle times (every
+// instance the reference builds): lane = device, the leaf scan and the phase-0 greedy exchange in
+// registers (the same choices as leaf_ranges + greedy_alloc: smallest increment first, ties to the
+// lowest device, runs taken while they beat the runner-up), then the incremental threshold scan.
+// Returns 1 solved (st0 = allocation), 0 infeasible, -1 not applicable (the table DP below runs).
+__device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, int lane, int64_t &nodes) {
+    const int M = I.M, R1 = I.R1, RS = I.RS;
+    const bool act = lane < M;
+    const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
+    int lo = R1, hi = -1, cnt = 0;
+    bool ok = true, mono = true;
+    double prev = kInf, dprev = -kInf, hprev = -kInf;
+    if (act)
+        for (int e = 0; e < R1; ++e) {
+            const double g = G[e], h = H[e];
+            if (g < kInf) {
+                if (cnt > 0) {
+                    const double d = g - prev;
+                    ok = ok && (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
+                    dprev = d;
+                }
+                mono = mono && h >= hprev;
+                hprev = h;
+                lo = min(lo, e);
+                hi = e;
+                prev = g;
+                ++cnt;
+            }
+        }
+    if (wave_or(act && (!ok || !mono))) return -1;
+    if (wave_or(act && cnt == 0)) return 0;
+    LeafInfo li;
+    li.convex = true;
+    li.mono = true;
+    li.empty = false;
+    li.lo_sum = wave_sum(act ? lo : 0);
+    li.cap = wave_sum(act ? hi - lo : 0);
+    li.my_lo = act ? lo : 0;
+    li.my_hi = act ? hi : -1;
+    int need = (R1 - 1) - li.lo_sum;
+    if (need < 0 || need > li.cap) return 0;
+    // phase 0: unconstrained greedy exchange (rounds: the smallest next increment wins and keeps
+    // every one still beating the runner-up)
+    int e = act ? lo : 0;
+    double inc = act && e < hi ? G[e + 1] - G[e] : kInf;
+    while (need > 0) {
+        const double bv = wave_min(inc);
+        const int win = lowest_lane(inc == bv);
+        const double rv = lane == win ? kInf : inc;
+        const double m2 = wave_min(rv);
+        const int d2 = lowest_lane(rv == m2);
+        const int t = take_run(w.G + int64_t(win) * RS, bcast(e, win), bcast(hi, win), need, m2, win < d2, lane);
+        if (lane == win) {
+            e += t;
+            inc = e < hi ? G[e + 1] - G[e] : kInf;
+        }
+        need -= t;
+    }
+    const double s_inf = wave_sum_f64(act ? G[e] : 0.0);
+    const double hmax = wave_max(act ? fmax(0.0, H[e]) : 0.0);
+    if (act) w.st0[lane] = e;
+    nodes = 1;
+    kc_scan_incremental(w, I, lane, s_inf, I.kc * hmax + s_inf, nodes, li);
+    wave_sync();
+    return 1;
+}
+
 // DP pass; k > 1: ascending threshold scan with bound pruning. One tree_dp call
 // site: phase 0 = unconstrained, 1 = threshold scan, 2 = final re-run. Leaves the
 // chosen e_i in st0; returns false when infeasible.
 __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &nodes) {
+#ifndef HALDA_NO_LANE_DP
+    if (I.kc > 0.0 && I.M >= 2 && I.M <= 64) {
+        const int r = dp_pass_lanes(w, I, lane, nodes);
+        if (r >= 0) return r == 1;
+    }
+#endif
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const double kc = I.kc;
     double *buf = kc > 0.0 ? w.work : w.G;
@@ -2754,7 +2843,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
             int rc = K1_FALLBACK, e = 0, rounds = 0;
             me.W = W;
             if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
-            if (k == 1 && regs && (!kTables || HALDA_SWEEP_TABLE_K1)) rc = k1_alloc(me, M, W - M, lane, e, rounds);
+            // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
+            // the solution for any k (the output adds (k - 1) max_i H_i)
+            if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M))
+                rc = k1_alloc(me, M, W - M, lane, e, rounds);
             if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
@@ -2798,6 +2890,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 return;
             } else {
                 Inst I = {};
+                I.inst = int(inst);
+                HALDA_TSTAMP(0);
                 I.M = M;
                 I.W = W;
                 I.Wd = double(W);
@@ -2809,9 +2903,11 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 int64_t nodes = 0;
                 if (M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab)) {
                     st = HALDA_STATUS_TOO_LARGE;  // beyond the launch's slice (the host sizes it from the fleets)
-                } else if (table_pass(src, w, I, lane), wave_sync(), !dp_pass(w, I, lane, nodes)) {
+                } else if (table_pass(src, w, I, lane), wave_sync(), [&] { HALDA_TSTAMP(6); return true; }(),
+                           !dp_pass(w, I, lane, nodes)) {
                     st = HALDA_STATUS_INFEASIBLE;
                 } else {
+                    HALDA_TSTAMP(7);
                     // solution: per device (w, n, least slacks, z), sum of costs, largest cycle time
                     double gs = 0.0, hmax = 0.0;
                     for (int i0 = 0; i0 < M; i0 += 64) {
@@ -2854,6 +2950,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                         if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
                         if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
                     }
+                    HALDA_TSTAMP(8);
                 }
                 wave_sync();  // tables / st0 are rewritten by the next k
             }
