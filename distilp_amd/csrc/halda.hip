@@ -2734,7 +2734,7 @@ __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fle
 struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
-    const int32_t *ks;
+    int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
     int n_k;
     halda_fleet_result out;
     int64_t xstride;
@@ -3140,6 +3140,8 @@ struct Ctx {
     size_t gtab_bytes = 0;
     hipEvent_t ev_order = nullptr;  // cross-stream ordering of consecutive launches on this context
     hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around a halda_solve_fleets sequence (lowering .. pick)
+    hipEvent_t evfm = nullptr;                   // fused sweep: between its first and second launch
+    bool fleet_two = false;                      // fused sweep: a second launch was enqueued
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool last_fleet_fused = false;
@@ -3341,6 +3343,8 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
 // launch for the fleets it flagged (gated on the hand-back flag); a batch whose k > 1 / wide
 // fleets need tables from the start gets the table launch only (LDS slice), or, beyond the LDS
 // budget, the register launch plus the global-table launch.
+constexpr int kSweepSmallBatch = 64;
+
 int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
                  const halda_fleet_result &out, hipStream_t s) {
     const int nf = F.n_fleets;
@@ -3369,12 +3373,10 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipMalloc(&c->fflag, need));
         c->fflag_bytes = need;
     }
-    int32_t *ks_dev = static_cast<int32_t *>(c->fflag);
-    HIP_TRY(hipMemcpyAsync(ks_dev, kh, sizeof(int32_t) * size_t(n_k), hipMemcpyHostToDevice, s));
     SweepArgs A = {};
     A.Mo = model;
     A.F = F;
-    A.ks = ks_dev;
+    for (int j = 0; j < n_k; ++j) A.ks[j] = kh[j];
     A.n_k = n_k;
     A.out = out;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
@@ -3388,7 +3390,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     c->fleet_timed = false;
     c->have_lowered = false;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    if (tables_first && fits) {
+    // small batches (a single halda_solve): one launch with the table slice instead of two
+    if (fits && (tables_first || nf <= kSweepSmallBatch)) {
         int per_cu = 0;
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
@@ -3399,6 +3402,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         A.want = 0;
         hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned(nf)), dim3(64), 0, s, A);
         HIP_TRY(hipGetLastError());
+        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;  // the fleets flagged above, gated on the hand-back flag
         if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
             int per_cu = 0;
@@ -3429,6 +3433,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
+    c->fleet_two = !(fits && (tables_first || nf <= kSweepSmallBatch));
     c->last_fleet_fused = true;
     return HALDA_OK;
 }
@@ -3481,7 +3486,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreate(&c->evf0) != hipSuccess || hipEventCreate(&c->evf1) != hipSuccess) {
+        hipEventCreate(&c->evf0) != hipSuccess || hipEventCreate(&c->evf1) != hipSuccess ||
+        hipEventCreate(&c->evfm) != hipSuccess) {
         halda_free(c);
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
@@ -3503,6 +3509,7 @@ void halda_free(void *ctx) {
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->evf0) (void)hipEventDestroy(c->evf0);
     if (c->evf1) (void)hipEventDestroy(c->evf1);
+    if (c->evfm) (void)hipEventDestroy(c->evfm);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evs) (void)hipEventDestroy(c->evs);
@@ -3571,30 +3578,37 @@ int halda_set_fleets_path(void *ctx, int fused) {
     return HALDA_OK;
 }
 
-int halda_last_fleet_ms(void *ctx, double *ms6) {
+int halda_last_fleet_ms(void *ctx, double *ms8) {
     Ctx *c = static_cast<Ctx *>(ctx);
-    if (!c || !ms6) return fail(HALDA_E_ARG, "NULL ctx/ms");
+    if (!c || !ms8) return fail(HALDA_E_ARG, "NULL ctx/ms");
     if (!c->fleet_timed) return fail(HALDA_E_ARG, "no timed halda_solve_fleets call on this context");
     HIP_TRY(hipEventSynchronize(c->evf1));
+    for (int i = 0; i < 8; ++i) ms8[i] = 0.0;
     if (c->last_fleet_fused) {
-        float t = 0.f;
-        HIP_TRY(hipEventElapsedTime(&t, c->evf0, c->evf1));
-        ms6[0] = t;
-        for (int i = 1; i < 6; ++i) ms6[i] = 0.0;
+        float a = 0.f, b = 0.f;
+        if (c->fleet_two) {
+            HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evfm));
+            HIP_TRY(hipEventElapsedTime(&b, c->evfm, c->evf1));
+            ms8[0] = a;
+            ms8[1] = b;
+        } else {
+            HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evf1));
+            ms8[1] = a;  // the table launch alone
+        }
         return HALDA_OK;
     }
+    if (!c->timed) return fail(HALDA_E_ARG, "no timed launch on this context");
     float lo = 0.f, a = 0.f, b = 0.f, d = 0.f, pk = 0.f;
     HIP_TRY(hipEventElapsedTime(&lo, c->evf0, c->ev0));
     HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evk));
     HIP_TRY(hipEventElapsedTime(&b, c->evk, c->evs));
     HIP_TRY(hipEventElapsedTime(&d, c->evs, c->ev1));
     HIP_TRY(hipEventElapsedTime(&pk, c->ev1, c->evf1));
-    ms6[0] = 0.0;
-    ms6[1] = lo;
-    ms6[2] = a;
-    ms6[3] = b;
-    ms6[4] = d;
-    ms6[5] = pk;
+    ms8[2] = lo;
+    ms8[3] = a;
+    ms8[4] = b;
+    ms8[5] = d;
+    ms8[6] = pk;
     return HALDA_OK;
 }
 

@@ -271,12 +271,12 @@ class HaldaContext:
 
     def last_fleet_ms(self) -> Dict[str, float]:
         """Device time of each launch of the last halda_solve_fleets call (zero entries dropped)."""
-        ms = (ctypes.c_double * 6)()
+        ms = (ctypes.c_double * 8)()
         rc = self.lib.halda_last_fleet_ms(self.ctx, ms)
         if rc != 0:
             raise RuntimeError(f"halda_last_fleet_ms failed ({rc}): {last_error(self.lib)}")
-        names = ("halda_sweep_kernel", "halda_lower_kernel", "halda_screen_kernel", "halda_solve_k1_kernel",
-                 "halda_solve_kernel", "halda_pick_kernel")
+        names = ("halda_sweep_kernel", "halda_sweep_tables_kernel", "halda_lower_kernel", "halda_screen_kernel",
+                 "halda_solve_k1_kernel", "halda_solve_kernel", "halda_pick_kernel", "reserved")
         return {n: float(v) for n, v in zip(names, ms) if v > 0.0}
 
     def last_phase_ms(self) -> Dict[str, float]:

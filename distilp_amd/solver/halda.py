@@ -110,8 +110,8 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                 c = np.array(res.c[0, j, :N])
                 t_comm, xi_sum, kappa = offsets
                 obj = float(c.dot(x)) + t_comm + xi_sum + kappa
-                r = ILPResult(k=k, w=[int(round(v)) for v in x[:M]], n=[int(round(v)) for v in x[M:2 * M]],
-                              obj_value=obj)
+                wn = np.rint(x[:2 * M]).astype(np.int64).tolist()  # int(round(v)): both round half to even
+                r = ILPResult(k=k, w=wn[:M], n=wn[M:], obj_value=obj)
             elif st != STATUS_INFEASIBLE:
                 raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
                                    "the lowered MILP does not have the HALDA structure")

@@ -202,10 +202,12 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
 int halda_set_fleets_path(void *ctx, int fused);
 
 /* Device time of the last halda_solve_fleets call per launch, in ms (per-launch events on, see
- * halda_set_timing): ms6[0] the fused sweep kernel (0 when the CSR pipeline ran), ms6[1] the lowering
- * kernel, ms6[2] the screen, ms6[3] the k = 1 solve, ms6[4] the general kernel's launches, ms6[5] the
- * pick kernel. */
-int halda_last_fleet_ms(void *ctx, double *ms6);
+ * halda_set_timing; 0 for launches that did not run): ms8[0] the fused sweep kernel
+ * (halda_sweep_kernel), ms8[1] its table launch (halda_sweep_tables_kernel / halda_sweep_big_kernel:
+ * the flagged fleets, or the whole batch when k > 1 / wide fleets need tables from the start);
+ * CSR pipeline: ms8[2] lowering, ms8[3] screen, ms8[4] k = 1 solve, ms8[5] general kernel,
+ * ms8[6] pick; ms8[7] reserved. */
+int halda_last_fleet_ms(void *ctx, double *ms8);
 
 /* Synchronous variant on HOST arrays (halda_fleets / halda_fleet_result in host
  * memory; obj_by_k and status may be NULL). */

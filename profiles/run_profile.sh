@@ -4,16 +4,16 @@
 # 1) rocprofv3 kernel trace + stats of the bench (same command as the bench line, fewer steps)
 # 2) two separate PMC passes (FETCH_SIZE, WRITE_SIZE) with kernel trace only, per MI355X_MICROARCH.md
 set -euo pipefail
-R=${1:-r01}
+R=${1:-r02}
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_$R
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-tto > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-tto > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
 # FETCH_SIZE calibration for 8-B and 16-B per-lane coalesced reads of a known byte count
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/calib" -o run -- \
     ./build/hbm_calib > "$OUT/calib.json" 2> "$OUT/calib.err"

@@ -19,8 +19,11 @@ REPO = Path(__file__).resolve().parent.parent
 
 
 def short(name):
-    """'(anonymous namespace)::halda_solve_k1_kernel(halda_batch, ...)' -> 'halda_solve_k1_kernel'."""
-    return name.split("(")[-2].split("::")[-1] if "::" in name else name.split("(")[0]
+    """'(anonymous namespace)::halda_sweep_kernel((anonymous namespace)::SweepArgs)' -> 'halda_sweep_kernel'."""
+    import re
+
+    m = re.search(r"(halda_\w+)\(", name)
+    return m.group(1) if m else name.split("(")[0]
 
 
 def per_kernel(csv_path, counter):
@@ -70,7 +73,8 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-    solve = out["kernels"].get("halda_screen_k1_kernel") or out["kernels"].get("halda_solve_k1_kernel")
+    solve = (out["kernels"].get("halda_sweep_kernel") or out["kernels"].get("halda_screen_k1_kernel")
+             or out["kernels"].get("halda_solve_k1_kernel"))
     out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
     out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
                    "coalesced read (tools/hbm_calib.hip), the solve kernel's dominant access width; "
