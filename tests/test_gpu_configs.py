@@ -189,3 +189,34 @@ def test_path_b_stub_on_reference_arrays(synth_golden, llama_online_model):
         obj = fl.objective_value(ref["c"], res.x)
         assert _close(obj, gold["obj_value"]), (key, obj, gold["obj_value"])
         assert (w, n) == (gold["w"], gold["n"]), key
+
+
+def test_c2_fleets_vs_exact_oracle(llama_online_model):
+    """C2 (BASELINE configs[1]): 256 synthetic 16-device fleets (seeds 0..255), every k of L = 80,
+    through halda_solve_fleets (the fused sweep: k = 1, 2, 4, 5 feasible) against the exact oracle
+    per (fleet, k) -- status, objective, (w, n) where unique -- and its k-sweep."""
+    tpl = load_templates()
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, 16, tpl)] for s in range(256)]
+    model = llama_online_model
+    res = solve_table(fleet_table(fleets, model), model, KS, 0.5, want_x=True)
+    n_unique = 0
+    for f, devs in enumerate(fleets):
+        best = None
+        for j, k in enumerate(KS):
+            p = mo.lower_dense(devs, model, k, 0.5)
+            st, xo, b1, b2, _ = mo.exact_solve(p)
+            if st == 2:
+                assert res.status[f, j] == STATUS_INFEASIBLE, (f, k)
+                continue
+            assert res.status[f, j] == STATUS_OPTIMAL, (f, k, res.status[f, j])
+            x = res.x[f, j, :p["c"].shape[0]]
+            assert _close(float(np.dot(p["c"], x)), b1), (f, k)
+            obj = mo.objective_value(p, x)
+            assert _close(float(res.obj_by_k[f, j]), obj)
+            if mo.uniqueness_margin_ok(b1, b2):
+                n_unique += 1
+                assert np.array_equal(x[:32], xo[:32]), (f, k)
+            if best is None or obj < best[0]:
+                best = (obj, k)
+        assert res.best_k[f] == best[1], f
+    assert n_unique >= 900
