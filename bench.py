@@ -133,10 +133,13 @@ def algorithmic_bytes(lowered, refs, n_k: int):
             screen += RES
             fused += scr + RES
             lower += 16 * M + 25 + 16
-    # fused k-sweep (no CSR): device fields in, per fleet best k / obj_value / w / n out
+    # fused k-sweep (no CSR): device fields in, per fleet best k / obj_value / w / n out -- the first
+    # launch (register or lane-segment kernel), or the table kernel when it runs the whole batch alone
+    # (as the dominant launch it does; as the gated second launch it only redoes flagged fleets)
     sweep = sum(DEV_FIELDS * fl.M + 8 + 4 + 8 + 8 * fl.M for fl in lowered)
     return {"halda_screen_k1_kernel": fused, "halda_screen_kernel": screen, "halda_solve_k1_kernel": solve,
-            "halda_lower_kernel": lower, "halda_pick_kernel": pick, "halda_sweep_kernel": sweep}
+            "halda_lower_kernel": lower, "halda_pick_kernel": pick, "halda_sweep_kernel": sweep,
+            "halda_sweep_seg_kernel": sweep, "halda_sweep_tables_kernel": sweep}
 
 
 # ------------------------------------------------------------------ CPU baseline

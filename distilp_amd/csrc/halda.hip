@@ -168,17 +168,6 @@ __device__ inline double wave_max(double v) { return __ockl_wfred_max_f64(v); }
 __device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
 __device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
 __device__ inline int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
-// Lowest / highest lane whose predicate holds (all lanes active), 0x7fffffff / -1 when none: a
-// ballot instead of a second wave reduction for the arg of a min / max.
-__device__ inline int lowest_lane(bool p) {
-    const uint64_t b = __ballot(p);
-    return b ? __builtin_ctzll(b) : 0x7fffffff;
-}
-__device__ inline int highest_lane(bool p) {
-    const uint64_t b = __ballot(p);
-    return b ? 63 - __builtin_clzll(b) : -1;
-}
-
 // Record of lane `src` broadcast to the whole wave (src wave-uniform).
 __device__ inline double bcast(double v, int src) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -192,6 +181,92 @@ __device__ inline double wave_sum_f64(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+
+// Row rotation of a 16-lane DPP row (row_ror:R, R = 1..15): lane i reads lane (i + R) mod 16 of its row.
+template <int R>
+__device__ inline int ror16(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x120 + R, 0xf, 0xf, false);
+}
+template <int R>
+__device__ inline double ror16(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = uint32_t(ror16<R>(int(uint32_t(u)))), hi = uint32_t(ror16<R>(int(uint32_t(u >> 32))));
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+// All-reduce over a 16-lane row by rotations 8, 4, 2, 1: after the first step a lane's value depends
+// on its index mod 8 only, so lane i's partner (i + 4) mod 16 holds what its xor partner i ^ 4 holds,
+// and so on: the same operands in the same order as the xor butterfly, and, op being commutative,
+// the same bits on every lane of the row.
+template <class T, class Op>
+__device__ inline T row16_reduce(T v, Op op) {
+    v = op(v, ror16<8>(v));
+    v = op(v, ror16<4>(v));
+    v = op(v, ror16<2>(v));
+    v = op(v, ror16<1>(v));
+    return v;
+}
+
+// Lanes per problem: Seg<64> = the whole wave (reductions, ballots and broadcasts as above);
+// Seg<16> = four problems per wave, each on a 16-lane DPP row (row rotations for the reductions,
+// ballots shifted to the row, broadcasts are bpermutes from the row). Sums over a 16-device problem
+// are bit-identical either way: the 64-lane xor butterfly first adds the zeros of lanes 16..63
+// (exact), then runs the steps 8, 4, 2, 1 that row16_reduce reproduces. Every lane of an active
+// segment must be active.
+template <int S_>
+struct Seg {
+    static_assert(S_ == 64 || S_ == 16, "a problem spans the wave or one 16-lane DPP row");
+    static constexpr int S = S_;
+    int sl, base;
+    __device__ explicit Seg(int lane) : sl(S_ == 64 ? lane : (lane & (S_ - 1))), base(S_ == 64 ? 0 : (lane & ~(S_ - 1))) {}
+    __device__ inline uint64_t bits(bool p) const {
+        const uint64_t b = __ballot(p);
+        if constexpr (S_ == 64) return b;
+        else return (b >> base) & ((uint64_t(1) << S_) - 1);
+    }
+    __device__ inline int lowest(bool p) const {
+        const uint64_t b = bits(p);
+        return b ? __builtin_ctzll(b) : 0x7fffffff;
+    }
+    __device__ inline int highest(bool p) const {
+        const uint64_t b = bits(p);
+        return b ? 63 - __builtin_clzll(b) : -1;
+    }
+    __device__ inline double min_f64(double v) const {
+        if constexpr (S_ == 64) return wave_min(v);
+        else return row16_reduce(v, [](double a, double b) { return fmin(a, b); });
+    }
+    __device__ inline double max_f64(double v) const {
+        if constexpr (S_ == 64) return wave_max(v);
+        else return row16_reduce(v, [](double a, double b) { return fmax(a, b); });
+    }
+    __device__ inline double sum_f64(double v) const {
+        if constexpr (S_ == 64) return wave_sum_f64(v);
+        else return row16_reduce(v, [](double a, double b) { return a + b; });
+    }
+    __device__ inline int sum_i(int v) const {
+        if constexpr (S_ == 64) return wave_sum(v);
+        else return row16_reduce(v, [](int a, int b) { return a + b; });
+    }
+    __device__ inline int or_i(int v) const {
+        if constexpr (S_ == 64) return wave_or(v);
+        else return row16_reduce(v, [](int a, int b) { return a | b; });
+    }
+    __device__ inline int imin(int v) const {
+        if constexpr (S_ == 64) return wave_imin(v);
+        else return row16_reduce(v, [](int a, int b) { return min(a, b); });
+    }
+    __device__ inline double bcast(double v, int src) const {
+        if constexpr (S_ == 64) return ::bcast(v, src);
+        else return __shfl(v, base + src);
+    }
+    __device__ inline int bcast(int v, int src) const {
+        if constexpr (S_ == 64) return ::bcast(v, src);
+        else return __shfl(v, base + src);
+    }
+    // value of the previous lane of the segment (its first lane: its own)
+    __device__ inline double up1(double v) const { return __shfl(v, base + (sl > 0 ? sl - 1 : 0)); }
+};
+using Wave = Seg<64>;
 
 
 __device__ inline void write_done(const halda_result &R, int inst, int status, int64_t nodes) {
@@ -590,15 +665,20 @@ __device__ LeafInfo leaf_ranges(const WaveCtx &w, int M, int R1, int RS, bool us
 // and a ballot instead of one dependent LDS round trip per increment; longer
 // runs continue in the next round (the winner is then the same device).
 // Returns the (wave-uniform) run length.
-__device__ inline int take_run(const double *G, int e0, int hi, int need, double m2, bool win_first, int lane) {
+template <class SG>
+__device__ inline int take_run(const double *G, int e0, int hi, int need, double m2, bool win_first, const SG &sg) {
     const int lim = min(need, hi - e0);
+    const int t = sg.sl;
     bool fail = true;
-    if (lane >= 1 && lane < lim) {
-        const double x = G[e0 + lane + 1] - G[e0 + lane];
+    if (t >= 1 && t < lim) {
+        const double x = G[e0 + t + 1] - G[e0 + t];
         fail = !(x < m2 || (x == m2 && win_first));
     }
-    const uint64_t nb = __ballot(lane >= 1 && fail);
-    return min(nb ? int(__builtin_ctzll(nb)) : 64, lim);
+    const uint64_t nb = sg.bits(t >= 1 && fail);
+    return min(nb ? int(__builtin_ctzll(nb)) : SG::S, lim);
+}
+__device__ inline int take_run(const double *G, int e0, int hi, int need, double m2, bool win_first, int lane) {
+    return take_run(G, e0, hi, need, m2, win_first, Wave(lane));
 }
 
 // Separable convex allocation by the greedy exchange: start every device at its
@@ -1067,10 +1147,10 @@ struct CsrSrc {
 // n*(w) is the same either way, so G and H are too.
 // src.load runs on every lane (index clamped to a valid device) so that a source may shuffle
 // records between lanes.
-template <class Src>
+template <int S = 64, class Src>
 __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int lane) {
-    if (I.M <= 32) {
-        const int P = 64 / I.M, chunk = (I.R1 + P - 1) / P;
+    if (I.M <= S / 2) {
+        const int P = S / I.M, chunk = (I.R1 + P - 1) / P;
         const int i = lane / P, p = lane - i * P;
         Dev d;
         src.load(d, w, min(i, I.M - 1));
@@ -1082,7 +1162,7 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
         }
         return;
     }
-    for (int i0 = 0; i0 < I.M; i0 += 64) {
+    for (int i0 = 0; i0 < I.M; i0 += S) {
         const int i = i0 + lane;
         Dev d;
         src.load(d, w, min(i, I.M - 1));
@@ -1109,11 +1189,13 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 // the pass-per-candidate scan: stop once (k-1) T + S(inf) >= best. Returns
 // false (caller runs the general scan) when a leaf is not convex / monotone.
 // On success st0 holds the allocation (table indices e_i).
-__device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, double s_inf, double best0,
+template <class SG>
+__device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &sg, double s_inf, double best0,
                                     int64_t &nodes, const LeafInfo &li0) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const double kc = I.kc;
-    if (M > 64 || M < 2 || !li0.convex || !li0.mono || li0.empty) return false;
+    const int lane = sg.sl;  // device index within the problem
+    if (M > SG::S || M < 2 || !li0.convex || !li0.mono || li0.empty) return false;
     HALDA_KSTAMP(3);
     const bool act = lane < M;
     const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
@@ -1121,7 +1203,7 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     const int need_total = (R1 - 1) - li0.lo_sum;
     if (need_total < 0 || need_total > li0.cap) return false;
     // start at T0 = max_i H_i(lo_i): every device can sit at its first allowed e
-    double T = wave_max(act ? H[lo] : -kInf);
+    double T = sg.max_f64(act ? H[lo] : -kInf);
     int cap = lo;
     if (act)
         while (cap < hi && H[cap + 1] <= T) ++cap;
@@ -1129,26 +1211,26 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     int e = lo;
     int need = need_total;
     {
-        const int avail = wave_sum(act ? cap - lo : 0);
+        const int avail = sg.sum_i(act ? cap - lo : 0);
         if (avail <= need) {  // take everything allowed (incomplete when avail < need)
             e = cap;
             need -= avail;
         } else {
             while (need > 0) {  // rounds: the smallest next increment wins and keeps every one beating the runner-up
                 const double nx = act && e < cap ? G[e + 1] - G[e] : kInf;
-                const double bv = wave_min(nx);
-                const int win = lowest_lane(nx == bv);
+                const double bv = sg.min_f64(nx);
+                const int win = sg.lowest(nx == bv);
                 const double rv = lane == win ? kInf : nx;
-                const double m2 = wave_min(rv);
-                const int d2 = lowest_lane(rv == m2);
-                const int t = take_run(w.G + int64_t(win) * RS, bcast(e, win), bcast(cap, win), need, m2, win < d2,
-                                       lane);
+                const double m2 = sg.min_f64(rv);
+                const int d2 = sg.lowest(rv == m2);
+                const int t = take_run(w.G + int64_t(win) * RS, sg.bcast(e, win), sg.bcast(cap, win), need, m2, win < d2,
+                                       sg);
                 if (lane == win) e += t;
                 need -= t;
             }
         }
     }
-    double S = wave_sum_f64(act ? G[e] : 0.0);
+    double S = sg.sum_f64(act ? G[e] : 0.0);
     HALDA_KSTAMP(4);
     double best = best0;
     int bestE = -1;
@@ -1165,8 +1247,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     double lam = -kInf;
     int lj = -1;
     if (need == 0) {
-        lam = wave_max(lt);
-        lj = highest_lane(lt == lam);
+        lam = sg.max_f64(lt);
+        lj = sg.highest(lt == lam);
         if (kc * T + S < best) {
             best = kc * T + S;
             bestE = e;
@@ -1175,11 +1257,11 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
     while (true) {
         const bool useful = act && e == cap && cap < hi && (need > 0 || gn < lam);
         const double cand = useful ? hn : kInf;
-        const double Tn = wave_min(cand);
+        const double Tn = sg.min_f64(cand);
         if (!(Tn < kInf) || !(kc * Tn + s_inf < best)) break;
-        const int li = lowest_lane(cand == Tn);
+        const int li = sg.lowest(cand == Tn);
         ++events;
-        const double d = bcast(gn, li);
+        const double d = sg.bcast(gn, li);
         const bool swap = need == 0;  // else: fill
         const int ljo = lj;
         S += swap ? d - lam : d;
@@ -1201,8 +1283,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
             lt = is_lj ? (e > lo ? Ge - Gm : -kInf) : Ge - Gm;
         }
         if (need == 0) {
-            lam = wave_max(lt);
-            lj = highest_lane(lt == lam);
+            lam = sg.max_f64(lt);
+            lj = sg.highest(lt == lam);
         }
         T = Tn;
         if (need == 0 && kc * T + S < best) {
@@ -1224,8 +1306,10 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, int lane, d
 // registers (the same choices as leaf_ranges + greedy_alloc: smallest increment first, ties to the
 // lowest device, runs taken while they beat the runner-up), then the incremental threshold scan.
 // Returns 1 solved (st0 = allocation), 0 infeasible, -1 not applicable (the table DP below runs).
-__device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, int lane, int64_t &nodes) {
+template <class SG>
+__device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int64_t &nodes) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
+    const int lane = sg.sl;
     const bool act = lane < M;
     const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
     int lo = R1, hi = -1, cnt = 0;
@@ -1248,14 +1332,14 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, int lane, int64_t 
                 ++cnt;
             }
         }
-    if (wave_or(act && (!ok || !mono))) return -1;
-    if (wave_or(act && cnt == 0)) return 0;
+    if (sg.or_i(act && (!ok || !mono))) return -1;
+    if (sg.or_i(act && cnt == 0)) return 0;
     LeafInfo li;
     li.convex = true;
     li.mono = true;
     li.empty = false;
-    li.lo_sum = wave_sum(act ? lo : 0);
-    li.cap = wave_sum(act ? hi - lo : 0);
+    li.lo_sum = sg.sum_i(act ? lo : 0);
+    li.cap = sg.sum_i(act ? hi - lo : 0);
     li.my_lo = act ? lo : 0;
     li.my_hi = act ? hi : -1;
     int need = (R1 - 1) - li.lo_sum;
@@ -1265,23 +1349,23 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, int lane, int64_t 
     int e = act ? lo : 0;
     double inc = act && e < hi ? G[e + 1] - G[e] : kInf;
     while (need > 0) {
-        const double bv = wave_min(inc);
-        const int win = lowest_lane(inc == bv);
+        const double bv = sg.min_f64(inc);
+        const int win = sg.lowest(inc == bv);
         const double rv = lane == win ? kInf : inc;
-        const double m2 = wave_min(rv);
-        const int d2 = lowest_lane(rv == m2);
-        const int t = take_run(w.G + int64_t(win) * RS, bcast(e, win), bcast(hi, win), need, m2, win < d2, lane);
+        const double m2 = sg.min_f64(rv);
+        const int d2 = sg.lowest(rv == m2);
+        const int t = take_run(w.G + int64_t(win) * RS, sg.bcast(e, win), sg.bcast(hi, win), need, m2, win < d2, sg);
         if (lane == win) {
             e += t;
             inc = e < hi ? G[e + 1] - G[e] : kInf;
         }
         need -= t;
     }
-    const double s_inf = wave_sum_f64(act ? G[e] : 0.0);
-    const double hmax = wave_max(act ? fmax(0.0, H[e]) : 0.0);
+    const double s_inf = sg.sum_f64(act ? G[e] : 0.0);
+    const double hmax = sg.max_f64(act ? fmax(0.0, H[e]) : 0.0);
     if (act) w.st0[lane] = e;
     nodes = 1;
-    kc_scan_incremental(w, I, lane, s_inf, I.kc * hmax + s_inf, nodes, li);
+    kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li);
     wave_sync();
     return 1;
 }
@@ -1292,7 +1376,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, int lane, int64_t 
 __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &nodes) {
 #ifndef HALDA_NO_LANE_DP
     if (I.kc > 0.0 && I.M >= 2 && I.M <= 64) {
-        const int r = dp_pass_lanes(w, I, lane, nodes);
+        const int r = dp_pass_lanes(w, I, Wave(lane), nodes);
         if (r >= 0) return r == 1;
     }
 #endif
@@ -1320,7 +1404,7 @@ __device__ bool dp_pass(const WaveCtx &w, const Inst &I, int lane, int64_t &node
             phase = 1;
             HALDA_KSTAMP(2);
             // convex leaves with monotone cycle times: one exchange per candidate T
-            if (kc_scan_incremental(w, I, lane, s_inf, best, nodes, li0)) return true;
+            if (kc_scan_incremental(w, I, Wave(lane), s_inf, best, nodes, li0)) return true;
             for (int i = lane; i < M; i += 64) {
                 double mn = kInf;
                 for (int e = 0; e < R1; ++e)
@@ -1565,13 +1649,6 @@ __device__ inline Dev bcast_dev(const Dev &d, int src) {
     return o;
 }
 
-__device__ inline double shfl_up1(double v, int lane) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const int src = lane > 0 ? lane - 1 : 0;
-    const uint32_t lo = __shfl(int(uint32_t(u)), src), hi = __shfl(int(uint32_t(u >> 32)), src);
-    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-}
-
 
 enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
 
@@ -1580,13 +1657,18 @@ enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
 struct FullRec {
     Dev d;
     __device__ inline Dev dev() const { return d; }
-    __device__ inline FullRec bcast(int src) const { return FullRec{bcast_dev(d, src)}; }
+    template <class SG>
+    __device__ inline FullRec bcast(const SG &, int src) const {
+        static_assert(SG::S == 64, "the CSR k = 1 path runs one problem per wave");
+        return FullRec{bcast_dev(d, src)};
+    }
 };
 
 // Greedy exchange over lazily evaluated convex leaves (lane = device, M <= 64).
 // On K1_OK, e holds the device's extra layers.
-template <class Rec>
-__device__ int k1_alloc(const Rec &rec, int M, int R, int lane, int &e, int &rounds) {
+template <class Rec, class SG>
+__device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int &rounds) {
+    const int lane = sg.sl;  // device index within the problem
     const Dev d = rec.dev();
     const bool act = lane < M;
     double g0 = kInf, g1 = kInf;
@@ -1598,7 +1680,7 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, int lane, int &e, int &rou
     }
     e = 0;
     // every leaf must start at e = 0 (a later start is legal but rare: general kernel)
-    if (wave_or(act && !ok0)) return K1_FALLBACK;
+    if (sg.or_i(act && !ok0)) return K1_FALLBACK;
     double gn = ok1 ? g1 : kInf;               // G(e + 1)
     double inc = ok1 ? g1 - g0 : kInf;        // G(e + 1) - G(e)
     double dprev = -kInf;                      // last taken increment (convexity check)
@@ -1606,43 +1688,43 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, int lane, int &e, int &rou
     rounds = 0;
     while (need > 0) {
         ++rounds;
-        const double bv = wave_min(act ? inc : kInf);
+        const double bv = sg.min_f64(act ? inc : kInf);
         if (!(bv < kInf)) return K1_INFEASIBLE;  // no device can take another layer
-        const int win = lowest_lane(act && inc == bv);
+        const int win = sg.lowest(act && inc == bv);
         const double rv = act && lane != win ? inc : kInf;
-        const double m2 = wave_min(rv);
-        const int d2 = lowest_lane(act && lane != win && rv == m2);
-        const int ew = bcast(e, win);
-        const double gnw = bcast(gn, win), dpw = bcast(dprev, win);
+        const double m2 = sg.min_f64(rv);
+        const int d2 = sg.lowest(act && lane != win && rv == m2);
+        const int ew = sg.bcast(e, win);
+        const double gnw = sg.bcast(gn, win), dpw = sg.bcast(dprev, win);
         // the winner takes its next increment bv; lane t evaluates G_win(ew + 2 + t)
         int take = 1;
         bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
         double Gt = kInf, dt = kInf;
         if (need > 1) {
-            const Dev dw = rec.bcast(win).dev();
+            const Dev dw = rec.bcast(sg, win).dev();
             const int wl = dw.wlo + ew + 2 + lane;
             double g = kInf;
             int nn = 0;
             if (wl <= dw.whi && split_full(dw, wl, g, nn, s)) Gt = g;
             // shuffles on the full wave first (a bpermute under a lane-0-off mask would read 0 there)
-            const double up = shfl_up1(Gt, lane);
+            const double up = sg.up1(Gt);
             const double prev = lane == 0 ? gnw : up;
             dt = Gt - prev;  // increment ew + 1 + lane -> ew + 2 + lane
-            const double dup = shfl_up1(dt, lane);
+            const double dup = sg.up1(dt);
             const double dlast = lane == 0 ? bv : dup;
             const bool fin = Gt < kInf && prev < kInf;
             const bool beats = fin && (dt < m2 || (dt == m2 && win < d2));
-            const uint64_t nb = __ballot(!beats);
-            const int run = nb ? __builtin_ctzll(nb) : 64;  // increments after the first that still win
-            take = min(min(1 + run, need), 64);
+            const uint64_t nb = sg.bits(!beats);
+            const int run = nb ? __builtin_ctzll(nb) : SG::S;  // increments after the first that still win
+            take = min(min(1 + run, need), SG::S);
             // convexity over the increments taken and the next one (they decide the exchange)
-            bad = bad || wave_or(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt)));
+            bad = bad || sg.or_i(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt)));
         }
         if (bad) return K1_FALLBACK;
         // winner's new state: e = ew + take; G(e) and G(e + 1) from the evaluated window
-        const double gcur = take == 1 ? gnw : bcast(Gt, take - 2);
-        const double gnext = need > 1 ? bcast(Gt, take - 1) : kInf;
-        const double tlast = take == 1 ? bv : bcast(dt, take - 2);
+        const double gcur = take == 1 ? gnw : sg.bcast(Gt, take - 2);
+        const double gnext = need > 1 ? sg.bcast(Gt, take - 1) : kInf;
+        const double tlast = take == 1 ? bv : sg.bcast(dt, take - 2);
         if (lane == win) {
             e = ew + take;
             gn = gnext;
@@ -1960,7 +2042,7 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_PSTAMP(3);
     HALDA_PSTAMP(4);
     int e = 0, rounds = 0;
-    const int rc = k1_alloc(FullRec{d}, I.M, I.W - sumlo, lane, e, rounds);
+    const int rc = k1_alloc(FullRec{d}, I.M, I.W - sumlo, Wave(lane), e, rounds);
     wave_sync();  // LDS records are rewritten by the next instance
     HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
@@ -2619,12 +2701,13 @@ struct FieldRec {
         o.W = W;
         return o;
     }
-    __device__ inline FieldRec bcast(int src) const {
+    template <class SG>
+    __device__ inline FieldRec bcast(const SG &sg, int src) const {  // the problem's device src, on every lane
         FieldRec o;
-        o.alpha = ::bcast(alpha, src); o.b = ::bcast(b, src); o.p_bp = ::bcast(p_bp, src);
-        o.p_b = ::bcast(p_b, src); o.cst = ::bcast(cst, src);
-        o.Kset = ::bcast(Kset, src); o.Kvram = ::bcast(Kvram, src);
-        const int cg = ::bcast(cls | (gpu << 4), src);
+        o.alpha = sg.bcast(alpha, src); o.b = sg.bcast(b, src); o.p_bp = sg.bcast(p_bp, src);
+        o.p_b = sg.bcast(p_b, src); o.cst = sg.bcast(cst, src);
+        o.Kset = sg.bcast(Kset, src); o.Kvram = sg.bcast(Kvram, src);
+        const int cg = sg.bcast(cls | (gpu << 4), src);
         o.cls = cg & 15; o.gpu = cg >> 4;
         o.W = W;
         return o;
@@ -2669,13 +2752,14 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, 
 struct FieldSrc {
     const halda_model *Mo;
     const halda_fleets *F;
-    const FieldRec *me;  // lane's own record (M <= 64), or nullptr
+    const FieldRec *me;  // lane's own record (M <= lanes per problem), or nullptr
     int64_t d0;
     int W;
+    int base;            // first lane of the problem's lane group
     __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
         FieldRec r;
         if (me) {
-            r = me->shfl(i);
+            r = me->shfl(base + i);
         } else {
             int bad = 0;
             r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
@@ -2701,15 +2785,17 @@ __device__ inline double kappa_head(const halda_model &Mo, int flags, double scp
     return total;
 }
 
-__device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, int lane, double &tsum,
+template <class SG>
+__device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
                                           double &xsum, double &kappa) {
-    const bool act = lane < M;
-    tsum = wave_sum_f64(act ? mf.tcomm : 0.0);
-    xsum = wave_sum_f64(act ? xi_term(mf) : 0.0);
-    const double tail = wave_sum_f64(act ? tail_term(mf) : 0.0);
-    int hi = lowest_lane(act && (mf.flags & HALDA_DEV_HEAD));
-    if (hi > 63) hi = 0;
-    kappa = kappa_head(Mo, bcast(mf.flags, hi), bcast(mf.scpu, hi), bcast(mf.Tc, hi), bcast(mf.sdisk, hi)) + tail;
+    const bool act = sg.sl < M;
+    tsum = sg.sum_f64(act ? mf.tcomm : 0.0);
+    xsum = sg.sum_f64(act ? xi_term(mf) : 0.0);
+    const double tail = sg.sum_f64(act ? tail_term(mf) : 0.0);
+    int hi = sg.lowest(act && (mf.flags & HALDA_DEV_HEAD));
+    if (hi >= SG::S) hi = 0;
+    kappa = kappa_head(Mo, sg.bcast(mf.flags, hi), sg.bcast(mf.scpu, hi), sg.bcast(mf.Tc, hi), sg.bcast(mf.sdisk, hi)) +
+            tail;
 }
 
 __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
@@ -2768,15 +2854,31 @@ __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, in
 #define HALDA_SWEEP_TABLE_K1 1  // table launches also run the k = 1 register greedy (else k = 1 via tables)
 #endif
 
-template <bool kTables, bool kGlobal>
-__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lane) {
+__device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
+    if (lane == 0) {
+        A.fflag[f] = 1;
+        __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// SG = Wave: one fleet per wave; SG = Seg<16>: one fleet (M <= 16, n_k <= 16) per 16-lane segment,
+// tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
+// only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
+// the one-fleet-per-wave table launch, as the register-only launch does.
+template <bool kTables, bool kGlobal, class SG = Wave>
+__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg) {
+    constexpr int S = SG::S;
+    constexpr bool kSeg = S < 64;
+    constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
+    const int lane = sg.sl;  // device index within the fleet
     const halda_model &Mo = A.Mo;
     const halda_fleets &F = A.F;
     HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
     const int64_t d0 = F.dev_off[f];
     const int M = int(F.dev_off[f + 1] - d0);
-    const bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
+    bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
+    if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
     FieldRec me = {};
     int bad = 0;
     double tsum = 0.0, xsum = 0.0, kappa = 0.0;
@@ -2785,7 +2887,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
         const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
         me = field_rec(Mo, mf, bad);
         bad = lane < M ? bad : 0;
-        if (M > 0) fleet_offsets_regs(Mo, mf, M, lane, tsum, xsum, kappa);
+        if (M > 0) fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
     } else {
         for (int i = lane; i < M; i += 64) {
             int b1 = 0;
@@ -2794,7 +2896,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
         }
         fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
     }
-    bad = wave_or(bad);
+    bad = sg.or_i(bad);
     HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
     double best = kInf;
     int best_k = 0;
@@ -2815,24 +2917,24 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
         if (A.out.status) A.out.status[inst] = stj;
     }
     if (A.out.x || A.out.c) {  // x / c of a settled instance are zero
-        uint64_t settled = __ballot(kl && stj != kOpen);
+        uint64_t settled = sg.bits(kl && stj != kOpen);
         const int N = 7 * M + 1;
         while (settled) {
             const int j = __builtin_ctzll(settled);
             settled &= settled - 1;
             const int64_t inst = int64_t(f) * A.n_k + j;
-            for (int cc = lane; cc < N; cc += 64) {
+            for (int cc = lane; cc < N; cc += S) {
                 if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
                 if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
             }
         }
     }
-    uint64_t todo = __ballot(kl && stj == kOpen);
+    uint64_t todo = sg.bits(kl && stj == kOpen);
     while (todo) {
         const int j = __builtin_ctzll(todo);
         todo &= todo - 1;
-        const int k = bcast(kj, j);
-        const int W = bcast(Wj, j);
+        const int k = sg.bcast(kj, j);
+        const int W = sg.bcast(Wj, j);
         const int64_t inst = int64_t(f) * A.n_k + j;
         const double kc = double(k - 1);
         int st;
@@ -2846,7 +2948,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
             // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
             // the solution for any k (the output adds (k - 1) max_i H_i)
             if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M))
-                rc = k1_alloc(me, M, W - M, lane, e, rounds);
+                rc = k1_alloc(me, M, W - M, sg, e, rounds);
             if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
@@ -2862,8 +2964,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                     z = Q > P ? 0.5 * (Q - P) : 0.0;
                     H = Q >= P ? 0.5 * (P + Q) : P;
                 }
-                const double hmax = fmax(0.0, wave_max(lane < M ? H : 0.0));
-                obj = wave_sum_f64(lane < M ? g : 0.0) + kc * hmax;
+                const double hmax = fmax(0.0, sg.max_f64(lane < M ? H : 0.0));
+                obj = sg.sum_f64(lane < M ? g : 0.0) + kc * hmax;
                 obj = obj + tsum;
                 obj = obj + xsum;
                 obj = obj + kappa;
@@ -2883,12 +2985,13 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
             } else if constexpr (!kTables) {
                 // k > 1, a wide fleet or a fast-path fallback: the table launch redoes this fleet
-                if (lane == 0) {
-                    A.fflag[f] = 1;
-                    __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                flag_fleet(A, f, lane);
                 return;
             } else {
+                if (kSeg && (kc == 0.0 || M < 2)) {  // a k = 1 fast-path fallback / one device: the 64-lane kernel
+                    flag_fleet(A, f, lane);
+                    return;
+                }
                 Inst I = {};
                 I.inst = int(inst);
                 HALDA_TSTAMP(0);
@@ -2899,18 +3002,38 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                 I.iC = 7 * M;
                 I.R1 = W - M + 1;
                 I.RS = odd_stride(I.R1);
-                const FieldSrc src{&A.Mo, &A.F, regs ? &me : nullptr, d0, W};
+                const FieldSrc src{&A.Mo, &A.F, regs ? &me : nullptr, d0, W, sg.base};
                 int64_t nodes = 0;
-                if (M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab)) {
+                const bool too_large =
+                    M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab);
+                if (kSeg && too_large) {
+                    flag_fleet(A, f, lane);
+                    return;
+                }
+                int feas = 1;
+                if (!too_large) {
+                    table_pass<S>(src, w, I, lane);
+                    wave_sync();
+                    HALDA_TSTAMP(6);
+                    if constexpr (kSeg) {
+                        feas = dp_pass_lanes(w, I, sg, nodes);
+                        if (feas < 0) {  // a leaf the incremental scan does not take
+                            flag_fleet(A, f, lane);
+                            return;
+                        }
+                    } else {
+                        feas = dp_pass(w, I, lane, nodes) ? 1 : 0;
+                    }
+                }
+                if (too_large) {
                     st = HALDA_STATUS_TOO_LARGE;  // beyond the launch's slice (the host sizes it from the fleets)
-                } else if (table_pass(src, w, I, lane), wave_sync(), [&] { HALDA_TSTAMP(6); return true; }(),
-                           !dp_pass(w, I, lane, nodes)) {
+                } else if (!feas) {
                     st = HALDA_STATUS_INFEASIBLE;
                 } else {
                     HALDA_TSTAMP(7);
                     // solution: per device (w, n, least slacks, z), sum of costs, largest cycle time
                     double gs = 0.0, hmax = 0.0;
-                    for (int i0 = 0; i0 < M; i0 += 64) {
+                    for (int i0 = 0; i0 < M; i0 += S) {
                         const int i = i0 + lane;
                         Dev d;
                         src.load(d, w, min(i, M - 1));
@@ -2925,15 +3048,15 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
                             put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
                         }
                     }
-                    hmax = wave_max(hmax);
-                    obj = wave_sum_f64(gs) + kc * hmax;
+                    hmax = sg.max_f64(hmax);
+                    obj = sg.sum_f64(gs) + kc * hmax;
                     obj = obj + tsum;
                     obj = obj + xsum;
                     obj = obj + kappa;
                     st = HALDA_STATUS_OPTIMAL;
                     improved = obj < best;
                     if (improved)
-                        for (int i0 = 0; i0 < M; i0 += 64) {
+                        for (int i0 = 0; i0 < M; i0 += S) {
                             const int i = i0 + lane;
                             Dev d;
                             src.load(d, w, min(i, M - 1));
@@ -2969,7 +3092,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
         }
         if (st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
             const int N = 7 * M + 1;
-            for (int cc = lane; cc < N; cc += 64) {
+            for (int cc = lane; cc < N; cc += S) {
                 if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
                 if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
             }
@@ -2983,10 +3106,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, int lan
     if (lane == 0) {
         A.out.best_k[f] = best_k;
         A.out.obj_value[f] = best;
-        if (!kTables) A.fflag[f] = 0;
+        if (kFirst) A.fflag[f] = 0;
     }
     if (best_k == 0)
-        for (int i = lane; i < M; i += 64) {
+        for (int i = lane; i < M; i += S) {
             A.out.w[d0 + i] = 0;
             A.out.n[d0 + i] = 0;
         }
@@ -3024,7 +3147,7 @@ __device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base)
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            sweep_fleet<kTables, kGlobal>(A, int(b + int64_t(bit) * S), w, lane);
+            sweep_fleet<kTables, kGlobal>(A, int(b + int64_t(bit) * S), w, Wave(lane));
         }
     }
 }
@@ -3044,6 +3167,41 @@ __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_ta
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_big_kernel(SweepArgs A) {
     sweep_body<true, true>(A, A.gtab + int64_t(blockIdx.x) * A.gstride);
+}
+
+// halda_sweep_seg_kernel: fleets of at most kSegLanes devices (C2: 16) with at most kSegLanes
+// k-candidates, 64 / kSegLanes fleets per wave, one per lane segment, each with an LDS slice of only
+// what the lane-parallel path touches: G and H (k > 1 tables, row stride RS) and st0. Every wave
+// reduction of the one-fleet-per-wave path becomes a segment butterfly (same order of additions:
+// the wave butterfly's first two steps only add zeros for M <= 16), so the results are the same
+// bits; what the segment path does not take is flagged for the gated halda_sweep_tables_kernel.
+constexpr int kSegLanes = 16;
+
+__host__ __device__ inline int64_t seg_slice_bytes(int mmax, int tab_kc) {
+    return 2 * align16(int64_t(tab_kc) * 8) + align16(int64_t(mmax) * 4);
+}
+
+#ifndef HALDA_SEG_WAVES_PER_SIMD
+#define HALDA_SEG_WAVES_PER_SIMD 2
+#endif
+
+__global__ __launch_bounds__(64, HALDA_SEG_WAVES_PER_SIMD) void halda_sweep_seg_kernel(SweepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int kPer = 64 / kSegLanes;
+    const int lane = threadIdx.x;
+    const Seg<kSegLanes> sg(lane);
+    const int seg = lane / kSegLanes;
+    const int64_t tb = align16(int64_t(A.tab_kc) * 8);
+    unsigned char *base = smem + int64_t(seg) * seg_slice_bytes(A.mmax, A.tab_kc);
+    WaveCtx w = {};
+    w.G = reinterpret_cast<double *>(base);
+    w.H = reinterpret_cast<double *>(base + tb);
+    w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+    const int nf = A.F.n_fleets;
+    for (int64_t b = int64_t(blockIdx.x) * kPer; b < nf; b += int64_t(gridDim.x) * kPer) {
+        const int64_t f = b + seg;
+        if (f < nf) sweep_fleet<true, false, Seg<kSegLanes>>(A, int(f), w, sg);
+    }
 }
 
 // halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
@@ -3142,8 +3300,10 @@ struct Ctx {
     hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around a halda_solve_fleets sequence (lowering .. pick)
     hipEvent_t evfm = nullptr;                   // fused sweep: between its first and second launch
     bool fleet_two = false;                      // fused sweep: a second launch was enqueued
+    bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
+    bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
     bool last_fleet_fused = false;
     void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
     size_t fflag_bytes = 0;
@@ -3390,8 +3550,27 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     c->fleet_timed = false;
     c->have_lowered = false;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    // small batches (a single halda_solve): one launch with the table slice instead of two
-    if (fits && (tables_first || nf <= kSweepSmallBatch)) {
+    // fleets of <= 16 devices needing k > 1 tables: the lane-segment launch (four fleets per wave),
+    // then the table launch for what it flagged
+    const int64_t seg_lds = seg_slice_bytes(mmax, int(tab_kc)) * (64 / kSegLanes);
+    const bool seg = c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
+                     nf > kSweepSmallBatch && seg_lds <= kLdsBudget;
+    if (seg) {
+        int per_cu = 0;
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_seg_kernel), seg_lds, &per_cu));
+        const int64_t nw = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nw)));
+        A.want = 0;
+        hipLaunchKernelGGL(halda_sweep_seg_kernel, dim3(grid), dim3(64), size_t(seg_lds), s, A);
+        HIP_TRY(hipGetLastError());
+        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
+        A.want = 1;
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
+        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(unsigned(std::min<int64_t>(c->cus, nf))), dim3(64),
+                           size_t(slice), s, A);
+        HIP_TRY(hipGetLastError());
+    } else if (fits && (tables_first || nf <= kSweepSmallBatch)) {
+        // small batches (a single halda_solve): one launch with the table slice instead of two
         int per_cu = 0;
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
@@ -3433,7 +3612,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = !(fits && (tables_first || nf <= kSweepSmallBatch));
+    c->fleet_two = seg || !(fits && (tables_first || nf <= kSweepSmallBatch));
+    c->fleet_seg = seg;
     c->last_fleet_fused = true;
     return HALDA_OK;
 }
@@ -3480,6 +3660,7 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->two_pass = !(tp && tp[0] == '0');
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
+    c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -3571,10 +3752,12 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
     return HALDA_OK;
 }
 
-int halda_set_fleets_path(void *ctx, int fused) {
+int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    c->fleets_fused = fused != 0;
+    if (path < 0 || path > 2) return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused) or 2 (fused, one fleet per wave)");
+    c->fleets_fused = path != 0;
+    c->seg_sweep = path == 1;
     return HALDA_OK;
 }
 
@@ -3589,7 +3772,7 @@ int halda_last_fleet_ms(void *ctx, double *ms8) {
         if (c->fleet_two) {
             HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evfm));
             HIP_TRY(hipEventElapsedTime(&b, c->evfm, c->evf1));
-            ms8[0] = a;
+            ms8[c->fleet_seg ? 7 : 0] = a;
             ms8[1] = b;
         } else {
             HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evf1));

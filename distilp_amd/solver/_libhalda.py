@@ -261,9 +261,16 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
-    def set_fleets_path(self, fused: bool) -> None:
-        """halda_solve_fleets on the fused sweep (True, default) or the CSR pipeline (False)."""
-        self.lib.halda_set_fleets_path(self.ctx, int(bool(fused)))
+    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2}
+
+    def set_fleets_path(self, path) -> None:
+        """halda_solve_fleets on the fused sweep ("fused" / True, default: four fleets per wave where
+        they have at most 16 devices), the fused sweep one fleet per wave ("wave") or the CSR
+        pipeline ("csr" / False)."""
+        code = self.FLEET_PATHS[path] if isinstance(path, str) else int(bool(path))
+        rc = self.lib.halda_set_fleets_path(self.ctx, code)
+        if rc != 0:
+            raise RuntimeError(f"halda_set_fleets_path failed ({rc}): {last_error(self.lib)}")
 
     def set_timing(self, on: bool) -> None:
         """Record (or not) the per-launch HIP events behind last_kernel_ms / last_phase_ms."""
@@ -276,7 +283,7 @@ class HaldaContext:
         if rc != 0:
             raise RuntimeError(f"halda_last_fleet_ms failed ({rc}): {last_error(self.lib)}")
         names = ("halda_sweep_kernel", "halda_sweep_tables_kernel", "halda_lower_kernel", "halda_screen_kernel",
-                 "halda_solve_k1_kernel", "halda_solve_kernel", "halda_pick_kernel", "reserved")
+                 "halda_solve_k1_kernel", "halda_solve_kernel", "halda_pick_kernel", "halda_sweep_seg_kernel")
         return {n: float(v) for n, v in zip(names, ms) if v > 0.0}
 
     def last_phase_ms(self) -> Dict[str, float]:

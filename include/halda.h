@@ -194,19 +194,23 @@ typedef struct halda_fleet_result {
 int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                        int32_t n_k, halda_fleet_result *out, void *stream);
 
-/* How halda_solve_fleets runs (default 1, or 0 when HALDA_FLEETS_PATH=csr is set at halda_init):
+/* How halda_solve_fleets runs (default 1; HALDA_FLEETS_PATH=csr / =wave at halda_init select 0 / 2):
  * 1 the fused sweep (halda_sweep_kernel: every (fleet, k) built in registers from the device
- *   fields, solved and compared in one wave per fleet; no MILP is materialised);
+ *   fields, solved and compared in one wave per fleet; no MILP is materialised); batches of more
+ *   than 64 fleets of at most 16 devices (and at most 16 k) that need k > 1 tables run four fleets
+ *   per wave (halda_sweep_seg_kernel, one per 16-lane segment);
+ * 2 the fused sweep, one fleet per wave only;
  * 0 the CSR pipeline (lowering kernel -> the halda_solve_batch kernels -> pick kernel), which also
- *   keeps the lowered batch for halda_last_lowered. Both give the same statuses, x and k. */
-int halda_set_fleets_path(void *ctx, int fused);
+ *   keeps the lowered batch for halda_last_lowered. All give the same statuses, x and k.
+ * HALDA_E_ARG for any other path. */
+int halda_set_fleets_path(void *ctx, int path);
 
 /* Device time of the last halda_solve_fleets call per launch, in ms (per-launch events on, see
  * halda_set_timing; 0 for launches that did not run): ms8[0] the fused sweep kernel
- * (halda_sweep_kernel), ms8[1] its table launch (halda_sweep_tables_kernel / halda_sweep_big_kernel:
+ * (halda_sweep_kernel), ms8[7] the segment kernel (halda_sweep_seg_kernel), ms8[1] their table launch (halda_sweep_tables_kernel / halda_sweep_big_kernel:
  * the flagged fleets, or the whole batch when k > 1 / wide fleets need tables from the start);
  * CSR pipeline: ms8[2] lowering, ms8[3] screen, ms8[4] k = 1 solve, ms8[5] general kernel,
- * ms8[6] pick; ms8[7] reserved. */
+ * ms8[6] pick. */
 int halda_last_fleet_ms(void *ctx, double *ms8);
 
 /* Synchronous variant on HOST arrays (halda_fleets / halda_fleet_result in host

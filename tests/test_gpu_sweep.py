@@ -105,3 +105,38 @@ def test_multi_device_context_equals_single(llama_online_model):
     for fi, devs in enumerate(fleets):  # x / c are defined on each fleet's 7 M + 1 columns
         N = 7 * len(devs) + 1
         assert np.array_equal(one.x[fi, :, :N], many.x[fi, :, :N]) and np.array_equal(one.c[fi, :, :N], many.c[fi, :, :N])
+
+
+def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model):
+    """halda_sweep_seg_kernel (four fleets of <= 16 devices per wave) against the one-fleet-per-wave
+    sweep on 300 fleets of 1..16 devices: the same bits everywhere (statuses, obj_by_k, x, c, best k,
+    obj_value, w, n). One-device fleets and k = 1 fast-path fallbacks are flagged by the segment
+    kernel and redone by the gated table launch; the CSR pipeline agrees too."""
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    sizes = [1 + (s * 7) % 16 for s in range(300)]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(11000 + s, M)] for s, M in enumerate(sizes)]
+    table = fleet_table(fleets, llama_online_model)
+    ctx = get_context(0)
+    seg = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+    ctx.set_timing(True)
+    try:
+        solve_table(table, llama_online_model, ks, 0.5)
+        assert "halda_sweep_seg_kernel" in ctx.last_fleet_ms()  # the segment launch ran
+        ctx.set_fleets_path("wave")
+        wave = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+        solve_table(table, llama_online_model, ks, 0.5)
+        assert "halda_sweep_seg_kernel" not in ctx.last_fleet_ms()
+    finally:
+        ctx.set_fleets_path("fused")
+        ctx.set_timing(False)
+    for f in ("status", "obj_by_k", "best_k", "obj_value", "w", "n"):
+        assert np.array_equal(getattr(seg, f), getattr(wave, f)), f
+    for fi, M in enumerate(sizes):
+        N = 7 * M + 1
+        assert np.array_equal(seg.x[fi, :, :N], wave.x[fi, :, :N]) and np.array_equal(seg.c[fi, :, :N], wave.c[fi, :, :N])
+    ctx.set_fleets_path("csr")
+    try:
+        csr = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+    finally:
+        ctx.set_fleets_path("fused")
+    _compare(table, seg, csr, ks)

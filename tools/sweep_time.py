@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--M", type=str, default="64,16")
     ap.add_argument("--fleets", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--paths", type=str, default="fused,csr")
+    ap.add_argument("--paths", type=str, default="fused,wave,csr")
     args = ap.parse_args()
     import torch
 
@@ -37,7 +37,7 @@ def main():
         dts = [DeviceFleetTable(table, model, KS, 0.5, dev) for _ in range(4)]
         ref = None
         for path in args.paths.split(","):
-            ctx.set_fleets_path(path == "fused")
+            ctx.set_fleets_path(path)
             for i in range(3):
                 dts[i % 4].launch(ctx, stream.cuda_stream)
             torch.cuda.synchronize(dev)
