@@ -83,6 +83,11 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
     } while (0)
 #define HALDA_TSTAMP(slot) do {} while (0)
 #endif
+#elif defined(HALDA_MARKS)  // asm listing only: phase markers for tools/asm_regions.py
+#define HALDA_SSTAMP(slot, v) asm volatile("; PHASE_MARK " #slot)
+#define HALDA_TSTAMP(slot) do {} while (0)
+#define HALDA_WSTAMP(slot, v) do {} while (0)
+#define HALDA_STAMP(k) do {} while (0)
 #else
 #define HALDA_SSTAMP(slot, v) \
     do {                      \
@@ -541,6 +546,11 @@ __device__ inline bool split_step(const Dev &d, int w, int n_prev, double &g, in
     return true;
 }
 
+// Record accessors shared by the solve code (Dev here; the k-sweep's FieldRec has its own
+// overloads, found by argument-dependent lookup where the templates are instantiated).
+__device__ inline int rec_wlo(const Dev &d) { return d.wlo; }
+__device__ inline int rec_whi(const Dev &d) { return d.whi; }
+
 struct WaveCtx {
     int2 *rows;    // [i][q] packed capacity rows
     double *cyc;   // [i] {r1w, r2w, rhs1, rhs2}
@@ -551,6 +561,7 @@ struct WaveCtx {
     double *inc;   // [i] next increment of device i (greedy exchange)
     double *G, *H, *work;
     uint16_t *split;
+    uint8_t *dparg;  // register sweep: the wave's arg-min strip of the k = 1 DP fallback (k1_dp)
 };
 
 // Device record: costs / decoded rows from LDS, integer bounds from the batch.
@@ -1119,12 +1130,13 @@ __device__ int check_rows(const WaveCtx &w, int M, int lane) {
 }
 
 // One table entry e of device i, continuing the chain state (n, have).
-__device__ inline void table_entry(const Dev &d, const WaveCtx &w, const Inst &I, int i, int e, int &n, bool &have) {
-    const int wl = d.wlo + e;
+template <class Rec>
+__device__ inline void table_entry(const Rec &d, const WaveCtx &w, const Inst &I, int i, int e, int &n, bool &have) {
+    const int wl = rec_wlo(d) + e;
     int s[4];
     double g = kInf, h = kInf;
     bool ok = false;
-    if (wl <= d.whi) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
+    if (wl <= rec_whi(d)) ok = have ? split_step(d, wl, n, g, n, s) : split_full(d, wl, g, n, s);
     if (ok && I.kc > 0.0) h = fmax(0.0, least_cycle(d, wl, n, s));
     have = ok;
     w.G[i * I.RS + e] = ok ? g : kInf;
@@ -1133,6 +1145,7 @@ __device__ inline void table_entry(const Dev &d, const WaveCtx &w, const Inst &I
 
 // Device records of an instance decoded from its CSR (load_dev).
 struct CsrSrc {
+    using Rec = Dev;
     const halda_batch *B;
     int64_t co;
     int M;
@@ -1152,7 +1165,7 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
     if (I.M <= S / 2) {
         const int P = S / I.M, chunk = (I.R1 + P - 1) / P;
         const int i = lane / P, p = lane - i * P;
-        Dev d;
+        typename Src::Rec d;
         src.load(d, w, min(i, I.M - 1));
         if (i < I.M) {
             int n = 0;
@@ -1164,7 +1177,7 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
     }
     for (int i0 = 0; i0 < I.M; i0 += S) {
         const int i = i0 + lane;
-        Dev d;
+        typename Src::Rec d;
         src.load(d, w, min(i, I.M - 1));
         if (i < I.M) {
             int n = 0;
@@ -1657,6 +1670,7 @@ enum { K1_OK = 0, K1_INFEASIBLE = 1, K1_FALLBACK = 2 };
 struct FullRec {
     Dev d;
     __device__ inline Dev dev() const { return d; }
+    __device__ inline const Dev &core() const { return d; }
     template <class SG>
     __device__ inline FullRec bcast(const SG &, int src) const {
         static_assert(SG::S == 64, "the CSR k = 1 path runs one problem per wave");
@@ -1669,14 +1683,15 @@ struct FullRec {
 template <class Rec, class SG>
 __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int &rounds) {
     const int lane = sg.sl;  // device index within the problem
-    const Dev d = rec.dev();
+    const auto &d = rec.core();  // Dev, or the compact record with its specialised split
     const bool act = lane < M;
     double g0 = kInf, g1 = kInf;
     int n0 = 0, n1 = 0, s[4];
     bool ok0 = false, ok1 = false;
     if (act) {
-        ok0 = d.wlo <= d.whi && split_full(d, d.wlo, g0, n0, s);
-        ok1 = ok0 && d.wlo + 1 <= d.whi && split_step(d, d.wlo + 1, n0, g1, n1, s);
+        const int wlo = rec_wlo(d), whi = rec_whi(d);
+        ok0 = wlo <= whi && split_full(d, wlo, g0, n0, s);
+        ok1 = ok0 && wlo + 1 <= whi && split_step(d, wlo + 1, n0, g1, n1, s);
     }
     e = 0;
     // every leaf must start at e = 0 (a later start is legal but rare: general kernel)
@@ -1701,11 +1716,11 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
         double Gt = kInf, dt = kInf;
         if (need > 1) {
-            const Dev dw = rec.bcast(sg, win).dev();
-            const int wl = dw.wlo + ew + 2 + lane;
+            const auto dw = rec.bcast(sg, win).core();
+            const int wl = rec_wlo(dw) + ew + 2 + lane;
             double g = kInf;
             int nn = 0;
-            if (wl <= dw.whi && split_full(dw, wl, g, nn, s)) Gt = g;
+            if (wl <= rec_whi(dw) && split_full(dw, wl, g, nn, s)) Gt = g;
             // shuffles on the full wave first (a bpermute under a lane-0-off mask would read 0 there)
             const double up = sg.up1(Gt);
             const double prev = lane == 0 ? gnw : up;
@@ -1767,6 +1782,56 @@ __device__ inline double shfl_f64(double v, int src) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
     const uint32_t lo = __shfl(int(uint32_t(u)), src), hi = __shfl(int(uint32_t(u >> 32)), src);
     return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+
+// k = 1 (and W = M) by an exact min-plus DP over the devices, for any leaf shape (lane = r, R + 1 <=
+// kDpLanes): the register sweep's own fallback for what the greedy exchange does not take (a leaf
+// that is not convex within its tolerance, or that does not start at lb), so that the register
+// launch needs no table launch behind it. V_i(r) = min_e V_{i-1}(r - e) + G_i(e), G_i(e) = the
+// device's least cost at w = lb + e (split_full), ties -> the smallest e; the arg-min of every
+// (i, r) goes to the wave's LDS strip (kDpLanes bytes per device) for the backtrack. On K1_OK, e
+// holds the device's extra layers, as from k1_alloc.
+constexpr int kDpLanes = 64;
+
+template <class Rec>
+__device__ int k1_dp(const Rec &rec, int M, int R, const Wave &sg, int &e, uint8_t *arg) {
+    const int lane = sg.sl;
+    double V = kInf;  // lane r: V_{i-1}(r)
+    for (int i = 0; i < M; ++i) {
+        const auto di = rec.bcast(sg, i).core();
+        double G = kInf, g = 0.0;
+        int nn = 0, s[4];
+        const int wl = rec_wlo(di) + lane;
+        if (lane <= R && wl <= rec_whi(di) && split_full(di, wl, g, nn, s)) G = g;
+        if (i == 0) {
+            V = G;
+            continue;
+        }
+        double best = kInf;
+        int be = 0;
+        for (int q = 0; q <= R; ++q) {
+            const double gq = sg.bcast(G, q);
+            const double vp = shfl_f64(V, lane >= q ? lane - q : 0);
+            const double c = vp + gq;
+            if (lane >= q && c < best) {
+                best = c;
+                be = q;
+            }
+        }
+        V = lane <= R ? best : kInf;
+        arg[i * kDpLanes + lane] = uint8_t(be);
+    }
+    if (!(sg.bcast(V, R) < kInf)) return K1_INFEASIBLE;
+    wave_sync();  // the strip is read across lanes
+    int r = R;
+    e = 0;
+    for (int i = M - 1; i >= 1; --i) {
+        const int ei = arg[i * kDpLanes + r];
+        if (lane == i) e = ei;
+        r -= ei;
+    }
+    if (lane == 0) e = r;
+    return K1_OK;
 }
 
 constexpr int kRpSlots = 5;  // row pointers rp[0 .. ncap] per lane: ncap <= 64 * 5 - 1
@@ -2712,7 +2777,111 @@ struct FieldRec {
         o.W = W;
         return o;
     }
+    __device__ inline const FieldRec &core() const { return *this; }
 };
+
+// The solve primitives on a FieldRec, specialised. The Dev that dev() expands a record to has two
+// live slacks: its class slack s_c >= w + Kset (class 3: w - n + Kset; s_c <= W) and the VRAM slack
+// t >= n + Kvram (t <= nhi), both priced pv = (class 2 ? p_b : p_bp), with 0 <= n <= min(w, nhi),
+// nhi = W on a GPU device, else 0; every other slack is pinned to 0 by its bounds. So split_full /
+// split_step / dev_cycle below visit the same candidates with the same tie rule as on dev() and give
+// the same bits: a pinned slack adds p * 0 = +0, which leaves any sum of terms >= +0 unchanged, and
+// where that term is NaN there (an infinite price of another class: inf * 0) the cost is NaN here.
+__device__ inline double rec_pv(const FieldRec &r) { return r.cls == 2 ? r.p_b : r.p_bp; }
+__device__ inline bool rec_own(const FieldRec &r) { return unsigned(r.cls - 1) < 3u; }
+__device__ inline bool rec_nanx(const FieldRec &r) { return r.p_bp == kInf || (r.p_b == kInf && r.cls != 2); }
+__device__ inline int rec_wlo(const FieldRec &) { return 1; }
+__device__ inline int rec_whi(const FieldRec &r) { return r.W; }
+
+// Feasible n-interval for w layers (n_interval on dev()); false when no n is feasible (also when
+// the class 1 / 2 slack, which does not depend on n, exceeds its bound).
+__device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) {
+    const bool hs = r.Kset != kNoRow;
+    const int nhi = r.gpu ? r.W : 0;
+    nL = r.cls == 3 && hs ? max(0, w + r.Kset - r.W) : 0;
+    nU = min(nhi, w);
+    if (r.Kvram != kNoRow) nU = min(nU, nhi - r.Kvram);
+    const bool setok = !(hs && (r.cls == 1 || r.cls == 2)) || max(0, w + r.Kset) <= r.W;
+    return nL <= nU && setok;
+}
+
+// dev_cost on dev() for (w, n) and the least slacks (sc = the class slack, t = VRAM).
+__device__ inline double rec_cost(const FieldRec &r, int w, int n, int sc, int t) {
+    const double pv = rec_pv(r);
+    double g = r.alpha * double(w);
+    g = g + r.b * double(n);
+    if (rec_own(r)) g = g + pv * double(sc);
+    g = g + pv * double(t);
+    return rec_nanx(r) ? __builtin_nan("") : g;
+}
+
+__device__ inline void rec_try(const FieldRec &r, int w, int nn, int nL, int nU, double &best, int &bn) {
+    nn = min(max(nn, nL), nU);
+    const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
+    const double g = rec_cost(r, w, nn, sc, t);
+    if (g < best || (g == best && nn < bn)) {
+        best = g;
+        bn = nn;
+    }
+}
+
+__device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
+    const int sc = max(0, w - (r.cls == 3 ? n : 0) + r.Kset);
+    s[0] = r.cls == 1 ? sc : 0;
+    s[1] = r.cls == 2 ? sc : 0;
+    s[2] = r.cls == 3 ? sc : 0;
+    s[3] = max(0, n + r.Kvram);
+}
+
+__device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    int nL, nU;
+    if (!rec_interval(r, w, nL, nU)) return false;
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, w, nL, nL, nU, best, bn);
+    rec_try(r, w, nU, nL, nU, best, bn);
+    if (r.cls == 3 && r.Kset != kNoRow) rec_try(r, w, w + r.Kset, nL, nU, best, bn);  // class-slack kink
+    if (r.Kvram != kNoRow) rec_try(r, w, -r.Kvram, nL, nU, best, bn);                  // VRAM kink
+    if (bn < 0) return false;
+    g = best;
+    n = bn;
+    rec_slacks(r, w, bn, s);
+    return true;
+}
+
+__device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &g, int &n, int s[4]) {
+    int nL, nU;
+    if (!rec_interval(r, w, nL, nU)) return false;
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, w, n_prev, nL, nU, best, bn);
+    rec_try(r, w, n_prev + 1, nL, nU, best, bn);
+    if (bn < 0) return false;
+    g = best;
+    n = bn;
+    rec_slacks(r, w, bn, s);
+    return true;
+}
+
+// dev_cycle on dev(): rows (alpha, alpha + p_bp) w + b n + slack terms <= -cst.
+__device__ inline void dev_cycle(const FieldRec &r, int w, int n, const int s[4], double &P, double &Q) {
+    const double pv = rec_pv(r);
+    const int sc = r.cls == 1 ? s[0] : r.cls == 2 ? s[1] : s[2];
+    const double t0 = r.b * double(n), tc = pv * double(sc), tv = pv * double(s[3]);
+    double a1 = r.alpha * double(w), a2 = (r.alpha + r.p_bp) * double(w);
+    a1 = a1 + t0; a2 = a2 + t0;
+    if (rec_own(r)) { a1 = a1 + tc; a2 = a2 + tc; }
+    a1 = a1 + tv; a2 = a2 + tv;
+    if (rec_nanx(r)) a1 = a2 = __builtin_nan("");
+    P = a1 - (-r.cst);
+    Q = a2 - (-r.cst);
+}
+
+__device__ inline double least_cycle(const FieldRec &r, int w, int n, const int s[4]) {
+    double P, Q;
+    dev_cycle(r, w, n, s, P, Q);
+    return Q >= P ? 0.5 * (P + Q) : P;
+}
 
 __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, int &bad) {
     FieldRec r;
@@ -2750,14 +2919,14 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, 
 // i's record (me), which other lanes fetch by shuffle; wider fleets rebuild it from the table.
 // load() runs on every lane (uniform control flow: the shuffles read every lane's registers).
 struct FieldSrc {
+    using Rec = FieldRec;
     const halda_model *Mo;
     const halda_fleets *F;
     const FieldRec *me;  // lane's own record (M <= lanes per problem), or nullptr
     int64_t d0;
     int W;
     int base;            // first lane of the problem's lane group
-    __device__ inline void load(Dev &d, const WaveCtx &, int i) const {
-        FieldRec r;
+    __device__ inline void load(FieldRec &r, const WaveCtx &, int i) const {
         if (me) {
             r = me->shfl(base + i);
         } else {
@@ -2765,7 +2934,6 @@ struct FieldSrc {
             r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
         }
         r.W = W;
-        d = r.dev();
     }
 };
 
@@ -2831,12 +2999,15 @@ struct SweepArgs {
     unsigned char *gtab;           // kGlobal: per-wave slices
     int64_t gstride;
     int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
+    int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
+    int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
 };
 
 // x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
 // by the lane of each device when the caller asked for them.
 __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
-                              const Dev &d) {
+                              const FieldRec &r) {
+    const Dev d = r.dev();
     if (A.out.x) {
         double *x = A.out.x + inst * A.xstride;
         x[i] = double(wl); x[M + i] = double(n);
@@ -2875,8 +3046,13 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     const halda_fleets &F = A.F;
     HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
-    const int64_t d0 = F.dev_off[f];
-    const int M = int(F.dev_off[f + 1] - d0);
+    // lane j: k_j (the k list travels in the kernel arguments; its load is issued with the fields')
+    const bool kl = lane < A.n_k;
+    const int kj = A.ks[kl ? lane : 0];
+    // the fleet's extent: with one fleet size for the batch, from the (uniform, scalar-cached)
+    // dev_off[0], so that the field loads are the wave's first vector round trip
+    const int64_t d0 = A.uM > 0 ? F.dev_off[0] + int64_t(f) * A.uM : F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
     bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
     if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
     FieldRec me = {};
@@ -2898,15 +3074,18 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     }
     bad = sg.or_i(bad);
     HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 1  // diagnostic build only: stop after the records
+    if (lane < M) A.out.n[d0 + lane] = me.Kset + me.Kvram + int(me.alpha + me.b + me.p_bp + me.p_b + me.cst) + bad + kj;
+    if (lane == 0) A.out.obj_value[f] = tsum + xsum + kappa;
+    return;
+#endif
     double best = kInf;
     int best_k = 0;
-    // lane j: k_j and W_j = L / k_j; the k's settled without a solve (the screen's verdicts: W >= 1e6
-    // unsupported, M > W bound-infeasible, rows decode rejects) are written lane-parallel, and the
-    // loop below visits only the others, in ascending k
+    const int Wj = kl ? Mo.L / kj : 0;  // W_j = L / k_j
+    // the k's settled without a solve (the screen's verdicts: W >= 1e6 unsupported, M > W
+    // bound-infeasible, rows decode rejects) are written lane-parallel, and the loop below visits only
+    // the others, in ascending k
     constexpr int kOpen = 1000;
-    const bool kl = lane < A.n_k;
-    const int kj = A.ks[kl ? lane : 0];
-    const int Wj = kl ? Mo.L / kj : 0;
     int stj = kOpen;
     if (!(Wj < 1000000)) stj = HALDA_STATUS_UNSUPPORTED;
     else if (M > Wj) stj = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
@@ -2947,20 +3126,31 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
             // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
             // the solution for any k (the output adds (k - 1) max_i H_i)
-            if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M))
-                rc = k1_alloc(me, M, W - M, sg, e, rounds);
+            if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M)) {
+                if constexpr (!kTables) {
+                    // the register launch solves its greedy fallbacks itself (exact DP, R + 1 <= kDpLanes)
+                    if (!A.k1dp) rc = k1_alloc(me, M, W - M, sg, e, rounds);
+                    if (rc == K1_FALLBACK && W - M < kDpLanes) rc = k1_dp(me, M, W - M, sg, e, w.dparg);
+                } else {
+                    rc = k1_alloc(me, M, W - M, sg, e, rounds);
+                }
+            }
             if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 2  // diagnostic build only: stop after the first greedy
+            if (lane < M) A.out.n[d0 + lane] = e + rc + rounds;
+            if (lane == 0) A.out.obj_value[f] = tsum + xsum + kappa;
+            return;
+#endif
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
             } else if (rc == K1_OK) {
                 double g = 0.0, H = 0.0, z = 0.0;
                 int n = 0, sl[4] = {0, 0, 0, 0};
                 const int wl = 1 + e;
-                const Dev md = me.dev();
                 if (lane < M) {
                     double P, Q;
-                    split_full(md, wl, g, n, sl);
-                    dev_cycle(md, wl, n, sl, P, Q);
+                    split_full(me, wl, g, n, sl);
+                    dev_cycle(me, wl, n, sl, P, Q);
                     z = Q > P ? 0.5 * (Q - P) : 0.0;
                     H = Q >= P ? 0.5 * (P + Q) : P;
                 }
@@ -2972,7 +3162,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 st = HALDA_STATUS_OPTIMAL;
                 improved = obj < best;
                 if (lane < M) {
-                    put_xc(A, inst, M, lane, wl, n, sl, z, md);
+                    put_xc(A, inst, M, lane, wl, n, sl, z, me);
                     if (improved) {
                         A.out.w[d0 + lane] = wl;
                         A.out.n[d0 + lane] = n;
@@ -3035,7 +3225,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                     double gs = 0.0, hmax = 0.0;
                     for (int i0 = 0; i0 < M; i0 += S) {
                         const int i = i0 + lane;
-                        Dev d;
+                        FieldRec d;
                         src.load(d, w, min(i, M - 1));
                         if (i < M) {
                             const int wl = 1 + w.st0[i];
@@ -3058,7 +3248,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                     if (improved)
                         for (int i0 = 0; i0 < M; i0 += S) {
                             const int i = i0 + lane;
-                            Dev d;
+                            FieldRec d;
                             src.load(d, w, min(i, M - 1));
                             if (i < M) {
                                 const int wl = 1 + w.st0[i];
@@ -3155,9 +3345,18 @@ __device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base)
 #ifndef HALDA_SWEEP_WAVES_PER_SIMD
 #define HALDA_SWEEP_WAVES_PER_SIMD 4  // occupancy target of the register-only sweep (as the k = 1 kernel)
 #endif
+constexpr int kSweepWavesPerBlock = 4;  // fleets per workgroup of the register-only sweep
 
-__global__ __launch_bounds__(64, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_kernel(SweepArgs A) {
-    sweep_body<false, false>(A, nullptr);
+// The register-only sweep: exactly one fleet per wave, kSweepWavesPerBlock waves per workgroup (a
+// quarter of the workgroups to dispatch); no loop, so no kernel argument stays live past its use.
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_kernel(SweepArgs A) {
+    // wave-uniform by construction; readfirstlane lets the compiler know (scalar fleet addressing)
+    const int f = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    if (f >= A.F.n_fleets) return;
+    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
+    WaveCtx w = {};
+    w.dparg = dparg[threadIdx.x >> 6];
+    sweep_fleet<false, false>(A, f, w, Wave(int(threadIdx.x & 63)));
 }
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
@@ -3304,6 +3503,7 @@ struct Ctx {
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
+    bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
     bool last_fleet_fused = false;
     void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
     size_t fflag_bytes = 0;
@@ -3544,6 +3744,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     A.hb_flag = c->hb_flag;
     A.launch_id = ++c->launch_id;
     A.mmax = mmax;
+    A.uM = F.min_devices == F.max_devices ? F.max_devices : 0;
+    A.k1dp = c->k1_force_dp ? 1 : 0;
     A.r1max = int(r1max);
     A.tab = int(tab);
     A.tab_kc = int(tab_kc);
@@ -3579,15 +3781,23 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipGetLastError());
     } else {
         A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned(nf)), dim3(64), 0, s, A);
+        hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
+                           dim3(64 * kSweepWavesPerBlock), 0, s, A);
         HIP_TRY(hipGetLastError());
         if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;  // the fleets flagged above, gated on the hand-back flag
-        if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
+        // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
+        // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
+        const bool gate = tables_first || r1_k1 > kDpLanes;
+        if (!gate) {
+        } else if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
             int per_cu = 0;
             HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-            const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tables_first ? int64_t(c->cus) * per_cu
-                                                                                   : int64_t(c->cus), nf)));
+            int grid = int(std::max<int64_t>(1, std::min<int64_t>(tables_first ? int64_t(c->cus) * per_cu
+                                                                             : int64_t(c->cus), nf)));
+#ifdef HALDA_DIAG_GATE_GRID1
+            grid = 1;  // diagnostic build only: launch cost of the gated kernel vs its grid
+#endif
             hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
         } else {
             A.gstride = (slice + 255) & ~int64_t(255);
@@ -3612,7 +3822,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = seg || !(fits && (tables_first || nf <= kSweepSmallBatch));
+    c->fleet_two = seg || (!(fits && (tables_first || nf <= kSweepSmallBatch)) && (tables_first || r1_k1 > kDpLanes));
     c->fleet_seg = seg;
     c->last_fleet_fused = true;
     return HALDA_OK;
@@ -3755,9 +3965,11 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
 int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    if (path < 0 || path > 2) return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused) or 2 (fused, one fleet per wave)");
+    if (path < 0 || path > 3)
+        return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave) or 3 (fused, k = 1 by DP)");
     c->fleets_fused = path != 0;
     c->seg_sweep = path == 1;
+    c->k1_force_dp = path == 3;
     return HALDA_OK;
 }
 

@@ -261,12 +261,13 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
-    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2}
+    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3}
 
     def set_fleets_path(self, path) -> None:
         """halda_solve_fleets on the fused sweep ("fused" / True, default: four fleets per wave where
-        they have at most 16 devices), the fused sweep one fleet per wave ("wave") or the CSR
-        pipeline ("csr" / False)."""
+        they have at most 16 devices), the fused sweep one fleet per wave ("wave"), the CSR
+        pipeline ("csr" / False), or (test path) the fused sweep with every k = 1 solve of its
+        register launch done by the exact DP it falls back to ("dp")."""
         code = self.FLEET_PATHS[path] if isinstance(path, str) else int(bool(path))
         rc = self.lib.halda_set_fleets_path(self.ctx, code)
         if rc != 0:

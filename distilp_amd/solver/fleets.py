@@ -5,9 +5,12 @@ the returned c and x with NumPy, exactly as the reference forms it;
 `halda_solve_fleets` below is the throughput / streaming entry on the same
 kernels (obj_value formed on the GPU). Fleets are packed into a
 `FleetTable` (one entry per device, the fields the reference's formulas read,
-dense_common.py:25-230), and libhalda lowers every (fleet, k) on the GPU
-(bit-identical CSR to `lower.lower_fleet`), solves it and keeps the best k by the
-reference's rule (ascending k, strict "<", halda_p_solver.py:407). Only the
+dense_common.py:25-230), and libhalda's fused sweep builds every (fleet, k) MILP's
+per-device records in registers from the table (the records decoding the lowered
+CSR would give; no MILP is materialised), solves it exactly and keeps the best k by
+the reference's rule (ascending k, strict "<", halda_p_solver.py:407); the CSR
+pipeline (GPU lowering bit-identical to `lower.lower_fleet`, then the milp()
+replacement kernels) stays behind `set_fleets_path("csr")`. Only the
 table goes over PCIe (~1.9 KB per 64-device fleet instead of ~160 KB of lowered
 MILPs), and re-profiled fleets (config C5) never touch per-device Python
 objects: `FleetTable.perturbed` rescales the table directly.

@@ -64,8 +64,9 @@ typedef struct halda_batch {
      *   max_tab    >= M * (R + 1)   over instances with c[C] == 0 (k == 1)
      *   max_tab_kc >= M * (R + 1)   over instances with c[C]  > 0 (k  > 1)
      * halda_solve_batch() (host pointers) computes them itself when all are 0.
-     * An instance exceeding them gets HALDA_STATUS_TOO_LARGE. Limits: R + 1 <= 128
-     * (layers beyond the per-device minimum), LDS per solve wave <= 160 KiB. */
+     * An instance exceeding them gets HALDA_STATUS_TOO_LARGE. No cap on R + 1 or M
+     * beyond the int32 shape fields: instances whose tables exceed the LDS budget
+     * are solved on global-memory tables (halda_solve_big_kernel). */
     int32_t max_cols;
     int32_t max_R1;
     int32_t max_tab;

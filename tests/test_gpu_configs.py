@@ -78,6 +78,15 @@ def test_c3_bench_fleets_vs_exact_oracle(llama_online_model):
                 n_unique += 1
                 assert np.array_equal(x[:128], xo[:128]), f
     assert n_unique >= 900
+    # the register launch's exact DP fallback (forced for every k = 1 solve) on the same fleets
+    ctx = get_context(0)
+    ctx.set_fleets_path("dp")
+    try:
+        dp = solve_table(fleet_table(fleets, model), model, KS, 0.5)
+    finally:
+        ctx.set_fleets_path(True)
+    assert np.array_equal(dp.best_k, sweep.best_k)
+    assert np.allclose(dp.obj_value, sweep.obj_value, rtol=1e-12, atol=0.0)
     # the oracle agrees that k > 1 is infeasible (a sample: every k of the first fleets)
     for devs in fleets[:4]:
         for k in KS[1:]:

@@ -140,3 +140,36 @@ def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model):
     finally:
         ctx.set_fleets_path("fused")
     _compare(table, seg, csr, ks)
+
+
+@pytest.mark.parametrize("sizes", [[64] * 160, [48, 64] * 80])
+def test_k1_dp_fallback_path_equals_greedy(llama_online_model, sizes):
+    """The register launch's own fallback for the k = 1 greedy (k1_dp, an exact min-plus DP over the
+    devices; it is why that launch needs no table launch behind it), forced for every k = 1 instance
+    by the "dp" path: the same statuses, best k and obj_value as the greedy exchange, and (w, n)
+    equal up to exact ties of the objective (fleets repeat device templates: swapping identical
+    devices ties). Uniform fleet sizes (dev_off from dev_off[0]) and mixed ones (dev_off[f])."""
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(9000 + s, M)] for s, M in enumerate(sizes)]
+    table = fleet_table(fleets, llama_online_model)
+    ctx = get_context(0)
+    greedy = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+    ctx.set_fleets_path("dp")
+    try:
+        dp = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
+    finally:
+        ctx.set_fleets_path(True)
+    assert np.array_equal(dp.status, greedy.status)
+    assert np.array_equal(dp.best_k, greedy.best_k)
+    assert (greedy.best_k == 1).all()
+    assert np.allclose(dp.obj_value, greedy.obj_value, rtol=1e-12, atol=1e-12)
+    n_same = 0
+    for f in range(table.n_fleets):
+        M = int(table.dev_off[f + 1] - table.dev_off[f])
+        N = 7 * M + 1
+        assert np.array_equal(dp.c[f, 0, :N], greedy.c[f, 0, :N])
+        xa, xb = dp.x[f, 0, :N], greedy.x[f, 0, :N]
+        ca, cb = float(np.dot(xa, greedy.c[f, 0, :N])), float(np.dot(xb, greedy.c[f, 0, :N]))
+        assert abs(ca - cb) <= 1e-12 * max(1.0, abs(cb)), f
+        n_same += bool(np.array_equal(xa[:2 * M], xb[:2 * M]))
+    assert n_same >= table.n_fleets // 4  # most fleets have a unique optimum

@@ -2,17 +2,17 @@
 
 Development aid: build an asm file whose HALDA_STAMP(k) sites are replaced by
 `asm volatile("; PHASE_MARK k")`, then
-    python tools/asm_regions.py /tmp/hm.s
-prints, per region, the VALU / SALU / LDS / VMEM instruction counts and the
+    python tools/asm_regions.py /tmp/hm.s [kernel name, default solve_kernel]
+(-DHALDA_MARKS builds such a listing of the fused sweep's HALDA_SSTAMP sites) prints, per region, the VALU / SALU / LDS / VMEM instruction counts and the
 number of branch labels (loop bodies are counted once)."""
 import re
 import sys
 from collections import Counter
 
 
-def main(path):
+def main(path, kernel="solve_kernel"):
     lines = open(path).read().splitlines()
-    start = next(i for i, l in enumerate(lines) if re.match(r"^_Z.*solve_kernel.*:", l))
+    start = next(i for i, l in enumerate(lines) if re.match(rf"^_Z.*{kernel}.*:", l))
     region, stats = "pre", {}
     for l in lines[start:]:
         m = re.search(r"PHASE_MARK (\d+)", l)
@@ -40,4 +40,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:])
