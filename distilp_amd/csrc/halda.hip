@@ -182,8 +182,39 @@ __device__ inline double bcast(double v, int src) {
 }
 __device__ inline int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 
+// v of lane i ^ 32 / i ^ 16 without LDS (gfx950 permlane swaps: a copy's upper half / odd rows
+// exchanged with the other copy's lower half / even rows).
+__device__ inline uint32_t xor32_u32(uint32_t v, int lane) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, true, false);
+    return (lane & 32) ? r[0] : r[1];
+}
+__device__ inline uint32_t xor16_u32(uint32_t v, int lane) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, true, false);
+    return (lane & 16) ? r[0] : r[1];
+}
+template <int O>
+__device__ inline double xor_cross(double v, int lane) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = O == 32 ? xor32_u32(uint32_t(u), lane) : xor16_u32(uint32_t(u), lane);
+    const uint32_t hi = O == 32 ? xor32_u32(uint32_t(u >> 32), lane) : xor16_u32(uint32_t(u >> 32), lane);
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+template <int R>
+__device__ inline double ror16(double v);
+
+// Sum over the wave in the xor-butterfly order (steps 32, 16, 8, 4, 2, 1; every lane gets the same
+// bits). The cross-row steps are permlane swaps; after them a lane's value depends on its index
+// mod 16 only, so the in-row steps are DPP row rotations by 8, 4, 2, 1, whose partner holds the xor
+// partner's value (see row16_reduce): the same operands in the same order as shuffles through
+// LDS, without the LDS round trips. Every lane must be active.
 __device__ inline double wave_sum_f64(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = int(__lane_id());
+    v = v + xor_cross<32>(v, lane);
+    v = v + xor_cross<16>(v, lane);
+    v = v + ror16<8>(v);
+    v = v + ror16<4>(v);
+    v = v + ror16<2>(v);
+    v = v + ror16<1>(v);
     return v;
 }
 
@@ -268,8 +299,16 @@ struct Seg {
         if constexpr (S_ == 64) return ::bcast(v, src);
         else return __shfl(v, base + src);
     }
-    // value of the previous lane of the segment (its first lane: its own)
-    __device__ inline double up1(double v) const { return __shfl(v, base + (sl > 0 ? sl - 1 : 0)); }
+    // value of the previous lane of the segment (its first lane: its own): DPP wave_shr:1 / row_shr:1
+    // with the lane's own value where there is no source lane
+    __device__ inline double up1(double v) const {
+        constexpr int ctrl = S_ == 64 ? 0x138 : 0x111;
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = uint32_t(u), hi = uint32_t(u >> 32);
+        const uint32_t l2 = uint32_t(__builtin_amdgcn_update_dpp(int(lo), int(lo), ctrl, 0xf, 0xf, false));
+        const uint32_t h2 = uint32_t(__builtin_amdgcn_update_dpp(int(hi), int(hi), ctrl, 0xf, 0xf, false));
+        return __builtin_bit_cast(double, (uint64_t(h2) << 32) | l2);
+    }
 };
 using Wave = Seg<64>;
 
@@ -1733,7 +1772,7 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
             const int run = nb ? __builtin_ctzll(nb) : SG::S;  // increments after the first that still win
             take = min(min(1 + run, need), SG::S);
             // convexity over the increments taken and the next one (they decide the exchange)
-            bad = bad || sg.or_i(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt)));
+            bad = bad || sg.bits(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt))) != 0;
         }
         if (bad) return K1_FALLBACK;
         // winner's new state: e = ew + take; G(e) and G(e + 1) from the evaluated window
@@ -2989,6 +3028,7 @@ struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
     int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
+    int32_t Ws[64];  // W = L / k per k (host integer division)
     int n_k;
     halda_fleet_result out;
     int64_t xstride;
@@ -3046,9 +3086,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     const halda_fleets &F = A.F;
     HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
-    // lane j: k_j (the k list travels in the kernel arguments; its load is issued with the fields')
+    // lane j: k_j and W_j = L / k_j (kernel arguments; their loads are issued with the fields')
     const bool kl = lane < A.n_k;
     const int kj = A.ks[kl ? lane : 0];
+    const int Wj = kl ? A.Ws[lane] : 0;
     // the fleet's extent: with one fleet size for the batch, from the (uniform, scalar-cached)
     // dev_off[0], so that the field loads are the wave's first vector round trip
     const int64_t d0 = A.uM > 0 ? F.dev_off[0] + int64_t(f) * A.uM : F.dev_off[f];
@@ -3074,14 +3115,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     }
     bad = sg.or_i(bad);
     HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(9, __builtin_amdgcn_s_memrealtime());
 #if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 1  // diagnostic build only: stop after the records
-    if (lane < M) A.out.n[d0 + lane] = me.Kset + me.Kvram + int(me.alpha + me.b + me.p_bp + me.p_b + me.cst) + bad + kj;
+    if (lane < M) A.out.n[d0 + lane] = me.Kset + me.Kvram + int(me.alpha + me.b + me.p_bp + me.p_b + me.cst) + bad + kj + Wj;
     if (lane == 0) A.out.obj_value[f] = tsum + xsum + kappa;
     return;
 #endif
     double best = kInf;
     int best_k = 0;
-    const int Wj = kl ? Mo.L / kj : 0;  // W_j = L / k_j
     // the k's settled without a solve (the screen's verdicts: W >= 1e6 unsupported, M > W
     // bound-infeasible, rows decode rejects) are written lane-parallel, and the loop below visits only
     // the others, in ascending k
@@ -3296,7 +3337,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     if (lane == 0) {
         A.out.best_k[f] = best_k;
         A.out.obj_value[f] = best;
-        if (kFirst) A.fflag[f] = 0;
+        if (kFirst && A.fflag) A.fflag[f] = 0;
     }
     if (best_k == 0)
         for (int i = lane; i < M; i += S) {
@@ -3353,6 +3394,12 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
     // wave-uniform by construction; readfirstlane lets the compiler know (scalar fleet addressing)
     const int f = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
     if (f >= A.F.n_fleets) return;
+#ifdef HALDA_SWEEP_STAGGER
+    {  // experiment: the waves sharing a SIMD start their loads one after another (slot = HW wave id)
+        const int slot = __builtin_amdgcn_s_getreg(4 | (3 << 11)) & 3;
+        for (int q = 0; q < slot; ++q) __builtin_amdgcn_s_sleep(HALDA_SWEEP_STAGGER);
+    }
+#endif
     __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
@@ -3578,8 +3625,11 @@ GenShape lds_shape(const GenShape &full, bool *big) {
 }
 
 // Device-side ordering across streams: the verdict bytes, the hand-back flag and the fleet scratch
-// are per context, so a launch on another stream than the previous one waits for everything
-// enqueued on that stream so far (same stream: stream order already serialises them).
+// are per context, so a launch that uses them on another stream than the previous such launch
+// waits for everything enqueued on that stream so far (same stream: stream order already
+// serialises them). A launch that touches none of them (the fused sweep's register launch when it
+// needs no table launch behind it) neither waits nor is waited for: independent batches on two
+// streams overlap on the device.
 int order_after_previous(Ctx *ctx, hipStream_t s) {
     if (ctx->have_last && ctx->last_stream != s) {
         HIP_TRY(hipEventRecord(ctx->ev_order, ctx->last_stream));
@@ -3724,6 +3774,20 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     const bool tables_first = tab_kc > 0 || mmax > kK1MaxM;
     const int64_t slice = make_slice(mmax, int(r1max), int(tab), int(tab_kc)).total;
     const bool fits = slice <= kLdsBudget;
+    // fleets of <= 16 devices needing k > 1 tables: the lane-segment launch (four fleets per wave),
+    // then the table launch for what it flagged
+    const int64_t seg_lds = seg_slice_bytes(mmax, int(tab_kc)) * (64 / kSegLanes);
+    const bool seg = c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
+                     nf > kSweepSmallBatch && seg_lds <= kLdsBudget;
+    const bool reg_mode = !seg && !(fits && (tables_first || nf <= kSweepSmallBatch));
+    // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
+    // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
+    const bool gate = tables_first || r1_k1 > kDpLanes;
+    const bool scratch = !(reg_mode && !gate);  // flags / hand-back flag of this context in use
+    if (scratch) {
+        const int rc = order_after_previous(c, s);
+        if (rc != HALDA_OK) return rc;
+    }
     // staging: ks and the per-fleet flags
     const size_t need = 256 + ((size_t(nf) + 255) & ~size_t(255));
     if (need > c->fflag_bytes) {
@@ -3736,11 +3800,14 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     SweepArgs A = {};
     A.Mo = model;
     A.F = F;
-    for (int j = 0; j < n_k; ++j) A.ks[j] = kh[j];
+    for (int j = 0; j < n_k; ++j) {
+        A.ks[j] = kh[j];
+        A.Ws[j] = kh[j] != 0 ? model.L / kh[j] : 0;
+    }
     A.n_k = n_k;
     A.out = out;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
-    A.fflag = static_cast<uint8_t *>(c->fflag) + 256;
+    A.fflag = scratch ? static_cast<uint8_t *>(c->fflag) + 256 : nullptr;
     A.hb_flag = c->hb_flag;
     A.launch_id = ++c->launch_id;
     A.mmax = mmax;
@@ -3752,11 +3819,6 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     c->fleet_timed = false;
     c->have_lowered = false;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    // fleets of <= 16 devices needing k > 1 tables: the lane-segment launch (four fleets per wave),
-    // then the table launch for what it flagged
-    const int64_t seg_lds = seg_slice_bytes(mmax, int(tab_kc)) * (64 / kSegLanes);
-    const bool seg = c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
-                     nf > kSweepSmallBatch && seg_lds <= kLdsBudget;
     if (seg) {
         int per_cu = 0;
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_seg_kernel), seg_lds, &per_cu));
@@ -3786,9 +3848,6 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipGetLastError());
         if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;  // the fleets flagged above, gated on the hand-back flag
-        // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
-        // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
-        const bool gate = tables_first || r1_k1 > kDpLanes;
         if (!gate) {
         } else if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
             int per_cu = 0;
@@ -3822,7 +3881,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = seg || (!(fits && (tables_first || nf <= kSweepSmallBatch)) && (tables_first || r1_k1 > kDpLanes));
+    c->fleet_two = seg || (reg_mode && gate);
     c->fleet_seg = seg;
     c->last_fleet_fused = true;
     return HALDA_OK;
@@ -4037,11 +4096,11 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     const int32_t *kh = ks;
     for (int j = 0; j < n_k; ++j)
         if (kh[j] < 1 || (j && kh[j] <= kh[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    if (c->fleets_fused && n_k <= 64) return sweep_fleets(c, *model, F, ks, n_k, *out, s);  // orders itself
     {
         const int rc = order_after_previous(c, s);  // fleet_scratch / last_lowered are per context
         if (rc != HALDA_OK) return rc;
     }
-    if (c->fleets_fused && n_k <= 64) return sweep_fleets(c, *model, F, ks, n_k, *out, s);
     const LowerDims D = lower_dims(F.max_devices, n_k);
     const int64_t n_inst = int64_t(F.n_fleets) * n_k;
     if (n_inst > (int64_t(1) << 30) || int64_t(F.n_fleets) * D.nnz > (int64_t(1) << 31) - 1)

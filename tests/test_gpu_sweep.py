@@ -173,3 +173,36 @@ def test_k1_dp_fallback_path_equals_greedy(llama_online_model, sizes):
         assert abs(ca - cb) <= 1e-12 * max(1.0, abs(cb)), f
         n_same += bool(np.array_equal(xa[:2 * M], xb[:2 * M]))
     assert n_same >= table.n_fleets // 4  # most fleets have a unique optimum
+
+
+def test_register_launches_overlap_on_two_streams(llama_online_model):
+    """The register launch of a C3-shaped batch touches no context scratch, so launches on two
+    streams do not wait for each other (bench: one batch's loads overlap the previous batch's
+    compute). Batches alternating over two streams, with a CSR-pipeline call (which does use the
+    scratch) between them, give the results of one synchronous call each."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    tables = [fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(s, 64)]
+                           for s in range(b * 160, b * 160 + 160)], llama_online_model) for b in range(2)]
+    want = [solve_table(t, llama_online_model, ks, 0.5) for t in tables]
+    dts = [DeviceFleetTable(t, llama_online_model, ks, 0.5, dev) for t in tables]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    for i in range(8):
+        dts[i % 2].launch(ctx, streams[i % 2].cuda_stream)
+        if i == 4:
+            ctx.set_fleets_path("csr")
+            try:
+                mid = solve_table(tables[1], llama_online_model, ks, 0.5)
+            finally:
+                ctx.set_fleets_path(True)
+            assert np.array_equal(mid.best_k, want[1].best_k) and np.array_equal(mid.w, want[1].w)
+    torch.cuda.synchronize(dev)
+    for d, w in zip(dts, want):
+        assert np.array_equal(d.out["best_k"].cpu().numpy(), w.best_k)
+        assert np.array_equal(d.out["w"].cpu().numpy(), w.w) and np.array_equal(d.out["n"].cpu().numpy(), w.n)
+        assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)

@@ -47,10 +47,15 @@ def main():
     print(f"fleets {n}  median wave life {np.median(tot):.0f} shader cycles")
     for j, nm in enumerate(names):
         print(f"  {nm:24s} median {np.median(d[:, j]):8.0f}  share {d[:, j].sum() / tot.sum():.3f}")
-    t0, t1 = st[:, 7], st[:, 8]
+    t0, t1, tr = st[:, 7], st[:, 8], st[:, 9]
     base = t0.min()
-    print(f"timeline (100 MHz ticks = 10 ns): start spread {np.percentile(t0 - base, [0, 50, 99, 100])}, "
-          f"end {np.percentile(t1 - base, [0, 50, 99, 100])}, life median {np.median(t1 - t0)}")
+    q = [0, 10, 50, 90, 99, 100]
+    print(f"timeline (100 MHz ticks = 10 ns), percentiles {q}:")
+    print(f"  wave start      {np.percentile(t0 - base, q)}")
+    print(f"  records done    {np.percentile(tr - base, q)}")
+    print(f"  wave end        {np.percentile(t1 - base, q)}")
+    print(f"  records phase   {np.percentile(tr - t0, q)}")
+    print(f"  after records   {np.percentile(t1 - tr, q)}")
 
 
 if __name__ == "__main__":
