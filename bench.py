@@ -341,6 +341,9 @@ def main():
     ap.add_argument("--fleets", type=int, default=C3_FLEETS, help="fleets per GPU per step (weak scaling)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="headline: weak (fleets per GPU fixed) or strong (4096 fleets in total)")
+    ap.add_argument("--streams", type=int, choices=(1, 2), default=2,
+                    help="streams the k-sweep steps alternate over (1: every launch serialised, e.g. for "
+                         "per-dispatch profiling)")
     ap.add_argument("--M", type=int, default=64)
     ap.add_argument("--copies", type=int, default=0, help="resident copies per leg (0: enough to exceed the MALL)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -405,7 +408,7 @@ def main():
     # the k-sweep steps alternate between two streams: consecutive batches are independent (own
     # tables and results), so one batch's field loads overlap the previous batch's compute tail
     stream2 = torch.cuda.Stream(dev)
-    srefs = [sref, stream2.cuda_stream]
+    srefs = [sref, stream2.cuda_stream] if args.streams == 2 else [sref, sref]
 
     # ---- headline: the k-sweep from resident device-field tables (rotating copies > the MALL)
     tbytes = DeviceFleetTable(table, model, ks, 0.5, dev).nbytes()

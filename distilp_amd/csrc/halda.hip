@@ -3546,6 +3546,7 @@ struct Ctx {
     hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around a halda_solve_fleets sequence (lowering .. pick)
     hipEvent_t evfm = nullptr;                   // fused sweep: between its first and second launch
     bool fleet_two = false;                      // fused sweep: a second launch was enqueued
+    bool fleet_reg_alone = false;                // fused sweep: the register launch alone
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
@@ -3882,6 +3883,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         c->fleet_timed = true;
     }
     c->fleet_two = seg || (reg_mode && gate);
+    c->fleet_reg_alone = reg_mode && !gate;
     c->fleet_seg = seg;
     c->last_fleet_fused = true;
     return HALDA_OK;
@@ -4047,7 +4049,7 @@ int halda_last_fleet_ms(void *ctx, double *ms8) {
             ms8[1] = b;
         } else {
             HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evf1));
-            ms8[1] = a;  // the table launch alone
+            ms8[c->fleet_reg_alone ? 0 : 1] = a;  // the register launch or the table launch alone
         }
         return HALDA_OK;
     }

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Profiling recipe used for profiles/<round>_*: run on the GPU box from the repo root.
 #   bash profiles/run_profile.sh r01
-# 1) rocprofv3 kernel trace + stats of the bench (same command as the bench line, fewer steps)
+# 1) rocprofv3 kernel trace + stats of the bench (same command as the bench line, fewer steps, and
+#    --streams 1 so that every dispatch's begin..end is its own: with two streams in flight the
+#    dispatches of consecutive batches overlap and their durations include each other)
 # 2) two separate PMC passes (FETCH_SIZE, WRITE_SIZE) with kernel trace only, per MI355X_MICROARCH.md
 set -euo pipefail
 R=${1:-r02}
@@ -9,7 +11,7 @@ OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_$R
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
+    python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --streams 1 > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-tto > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_write" -o run -- \
