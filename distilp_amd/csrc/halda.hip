@@ -3543,6 +3543,7 @@ struct Ctx {
     void *gtab = nullptr;  // per-wave global-memory slices of the big-table general launch
     size_t gtab_bytes = 0;
     hipEvent_t ev_order = nullptr;  // cross-stream ordering of consecutive launches on this context
+    hipEvent_t ev_host = nullptr;   // completion of a small synchronous call (polled, not waited on)
     hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around a halda_solve_fleets sequence (lowering .. pick)
     hipEvent_t evfm = nullptr;                   // fused sweep: between its first and second launch
     bool fleet_two = false;                      // fused sweep: a second launch was enqueued
@@ -3780,7 +3781,10 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     const int64_t seg_lds = seg_slice_bytes(mmax, int(tab_kc)) * (64 / kSegLanes);
     const bool seg = c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
                      nf > kSweepSmallBatch && seg_lds <= kLdsBudget;
-    const bool reg_mode = !seg && !(fits && (tables_first || nf <= kSweepSmallBatch));
+    // small batches (a single halda_solve) take one launch: the register kernel when it needs no table
+    // launch behind it, else the table kernel alone
+    const bool small_tables = nf <= kSweepSmallBatch && r1_k1 > kDpLanes;
+    const bool reg_mode = !seg && !(fits && (tables_first || small_tables));
     // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
     // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
     const bool gate = tables_first || r1_k1 > kDpLanes;
@@ -3834,7 +3838,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(unsigned(std::min<int64_t>(c->cus, nf))), dim3(64),
                            size_t(slice), s, A);
         HIP_TRY(hipGetLastError());
-    } else if (fits && (tables_first || nf <= kSweepSmallBatch)) {
+    } else if (fits && (tables_first || small_tables)) {
         // small batches (a single halda_solve): one launch with the table slice instead of two
         int per_cu = 0;
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
@@ -3938,6 +3942,7 @@ int halda_init(int device_ordinal, void **ctx_out) {
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_host, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->evf0) != hipSuccess || hipEventCreate(&c->evf1) != hipSuccess ||
         hipEventCreate(&c->evfm) != hipSuccess) {
         halda_free(c);
@@ -3959,6 +3964,7 @@ void halda_free(void *ctx) {
     if (c->gtab) (void)hipFree(c->gtab);
     if (c->fflag) (void)hipFree(c->fflag);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    if (c->ev_host) (void)hipEventDestroy(c->ev_host);
     if (c->evf0) (void)hipEventDestroy(c->evf0);
     if (c->evf1) (void)hipEventDestroy(c->evf1);
     if (c->evfm) (void)hipEventDestroy(c->evfm);
@@ -4209,6 +4215,8 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
 }
 
 // Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.
+constexpr size_t kZeroCopyBytes = size_t(1) << 20;
+
 int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fh, const int32_t *ks,
                             int32_t n_k, halda_fleet_result *out_h) {
     Ctx *c = static_cast<Ctx *>(ctx);
@@ -4262,7 +4270,17 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
         if (!i64[a]) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
         HIP_TRY(up(o_i64 + 8 * nd * a, i64[a], 8 * nd));
     }
-    HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));
+    // small calls (a single halda_solve: ~8 KB in, ~70 KB out) skip both copies: the kernels read the
+    // table from and write the results to the pinned buffer itself, across PCIe, and the host polls
+    // the completion event instead of sleeping in a stream synchronisation
+    const bool zc = off <= kZeroCopyBytes;
+    if (zc) {
+        void *dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
+        base = static_cast<char *>(dp);
+    } else {
+        HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));
+    }
     auto F64 = [&](int a) { return reinterpret_cast<const double *>(base + o_f64 + 8 * nd * a); };
     auto I64 = [&](int a) { return reinterpret_cast<const int64_t *>(base + o_i64 + 8 * nd * a); };
     d.dev_off = reinterpret_cast<const int64_t *>(base + o_doff);
@@ -4283,8 +4301,16 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     r.c = out_h->c ? reinterpret_cast<double *>(base + o_c) : nullptr;
     const int rc = halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
     if (rc != HALDA_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(pin + o_bk, base + o_bk, off - o_bk, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (zc) {
+        HIP_TRY(hipEventRecord(c->ev_host, s));
+        hipError_t q;
+        while ((q = hipEventQuery(c->ev_host)) == hipErrorNotReady) {
+        }
+        HIP_TRY(q);
+    } else {
+        HIP_TRY(hipMemcpyAsync(pin + o_bk, base + o_bk, off - o_bk, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     auto down = [&](void *dst, size_t o, size_t bytes) {
         if (dst) std::memcpy(dst, pin + o, bytes);
         return hipSuccess;
@@ -4297,7 +4323,6 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     HIP_TRY(down(out_h->status, o_st, 4 * nf * n_k));
     HIP_TRY(down(out_h->x, o_x, 8 * xs));
     HIP_TRY(down(out_h->c, o_c, 8 * xs));
-    HIP_TRY(hipStreamSynchronize(s));
     return HALDA_OK;
 }
 

@@ -179,9 +179,42 @@ def _rate(table, q, f_has_b1: bool, raise_on_missing: bool) -> tuple:
     return True, float(row["b_1"])
 
 
+def _load_packer():
+    """The C packer (distilp_amd/csrc/fleetpack.c, built in-tree next to this file by build())."""
+    try:
+        from . import _fleetpack
+    except ImportError:
+        return None
+    return _fleetpack
+
+
+_PACKER = _load_packer()
+
+
 def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
-    """Pack fleets (lists of DeviceProfile) into a FleetTable (one row tuple per device, then one
-    NumPy conversion per field group)."""
+    """Pack fleets (lists of DeviceProfile) into a FleetTable: one pass of the C packer over the
+    devices into three field blocks (f64 [10][nd], int64 [6][nd], uint8 [2][nd]); the table's fields
+    are rows of those blocks. Same values, flags and exceptions as fleet_table_py."""
+    if _PACKER is None:
+        raise ImportError("distilp_amd/solver/_fleetpack.so is not built (run __graft_entry__.build())")
+    fleets = fleets if isinstance(fleets, (list, tuple)) else list(fleets)
+    nf = len(fleets)
+    nd = sum(len(d) for d in fleets)
+    f64 = np.empty((len(F64_FIELDS), nd), np.float64)
+    i64 = np.empty((len(I64_FIELDS), nd), np.int64)
+    u8 = np.empty((2, nd), np.uint8)
+    off = np.empty(nf + 1, np.int64)
+    heads = np.empty(nf, np.int64)
+    _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, i64, u8, off, heads)
+    t = FleetTable(dev_off=off, os_class=u8[0], flags=u8[1], **{f: f64[j] for j, f in enumerate(F64_FIELDS)},
+                   **{f: i64[j] for j, f in enumerate(I64_FIELDS)})
+    t._blocks = (off, u8, f64, i64)  # FleetTable.check ran in the packer
+    return t
+
+
+def fleet_table_py(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
+    """The packer in Python (one row tuple per device, then one NumPy conversion per field group):
+    the specification the C packer is tested against."""
     Q = model.Q
     fq, fout = "b_1" in model.f_q, "b_1" in model.f_out
     cls, flags, f64, i64, heads = [], [], [], [], []
@@ -265,6 +298,33 @@ def _fleets_struct(t: FleetTable, ptr) -> HaldaFleetsC:
     return s
 
 
+def _host_struct(t: FleetTable) -> tuple:
+    """(HaldaFleetsC on the table's host arrays, arrays to keep alive). A packed table's fields are
+    rows of three blocks: four pointer reads instead of one per field."""
+    blocks = getattr(t, "_blocks", None)
+    if blocks is None:
+        arrs = {f: np.ascontiguousarray(getattr(t, f)) for f in ("dev_off", "os_class", "flags") + F64_FIELDS
+                + I64_FIELDS}
+        return _fleets_struct(t, lambda f: arrs[f].ctypes.data), arrs
+    off, u8, f64, i64 = blocks
+    nd = u8.shape[1]
+    s = HaldaFleetsC()
+    s.n_fleets = t.n_fleets
+    if t.n_fleets == 1:
+        s.min_devices = s.max_devices = nd
+    else:
+        sz = np.diff(off)
+        s.min_devices, s.max_devices = int(sz.min()), int(sz.max())
+    s.dev_off = off.ctypes.data
+    pu, pf, pi = u8.ctypes.data, f64.ctypes.data, i64.ctypes.data
+    s.os_class, s.flags = pu, pu + nd
+    for j, f in enumerate(F64_FIELDS):
+        setattr(s, f, pf + 8 * nd * j)
+    for j, f in enumerate(I64_FIELDS):
+        setattr(s, f, pi + 8 * nd * j)
+    return s, blocks
+
+
 def _k_list(model: ModelProfile, k_candidates: Optional[Iterable[int]]) -> List[int]:
     if k_candidates:
         return sorted(set(int(k) for k in k_candidates))
@@ -313,19 +373,21 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
         raise ZeroDivisionError("integer division or modulo by zero")
     ctx = get_context(device) if _multi is None else None
     lib = _bind(ctx.lib) if _multi is None else _multi.lib
-    arrs = {f: np.ascontiguousarray(getattr(table, f)) for f in ("dev_off", "os_class", "flags") + F64_FIELDS
-            + I64_FIELDS}
-    fs = _fleets_struct(table, lambda f: arrs[f].ctypes.data)
+    fs, keep = _host_struct(table)
     nf, nd, nk = table.n_fleets, table.n_devices, len(ks)
-    out = FleetSolve(best_k=np.zeros(nf, np.int32), obj_value=np.zeros(nf), w=np.zeros(nd, np.int32),
-                     n=np.zeros(nd, np.int32), obj_by_k=np.zeros((nf, nk)), status=np.zeros((nf, nk), np.int32),
-                     ks=ks)
+    # results in two buffers (f64, int32) viewed per field: two pointer reads
+    xs = 7 * int(fs.max_devices) + 1 if want_x else 0
+    fbuf = np.zeros(nf + nf * nk + 2 * nf * nk * xs)
+    ibuf = np.zeros(nf + 2 * nd + nf * nk, np.int32)
+    pf, pi = fbuf.ctypes.data, ibuf.ctypes.data
+    o1, o2 = nf, nf + nf * nk
+    out = FleetSolve(best_k=ibuf[:nf], obj_value=fbuf[:nf], w=ibuf[nf:nf + nd], n=ibuf[nf + nd:nf + 2 * nd],
+                     obj_by_k=fbuf[o1:o2].reshape(nf, nk), status=ibuf[nf + 2 * nd:].reshape(nf, nk), ks=ks)
     if want_x:
-        xs = 7 * int(fs.max_devices) + 1
-        out.x, out.c = np.zeros((nf, nk, xs)), np.zeros((nf, nk, xs))
-    r = HaldaFleetResultC(out.best_k.ctypes.data, out.obj_value.ctypes.data, out.w.ctypes.data, out.n.ctypes.data,
-                          out.obj_by_k.ctypes.data, out.status.ctypes.data,
-                          out.x.ctypes.data if want_x else None, out.c.ctypes.data if want_x else None)
+        out.x = fbuf[o2:o2 + nf * nk * xs].reshape(nf, nk, xs)
+        out.c = fbuf[o2 + nf * nk * xs:].reshape(nf, nk, xs)
+    r = HaldaFleetResultC(pi, pf, pi + 4 * nf, pi + 4 * (nf + nd), pf + 8 * o1, pi + 4 * (nf + 2 * nd),
+                          pf + 8 * o2 if want_x else None, pf + 8 * (o2 + nf * nk * xs) if want_x else None)
     karr = np.asarray(ks, np.int32)
     m = model_struct(model, kv_factor)
     if _multi is not None:

@@ -142,3 +142,40 @@ def test_halda_solve_raises_where_the_reference_loop_does(llama_online_model, ca
     with pytest.raises(ValueError, match="b_1"):
         halda_solve(bad, llama_online_model, k_candidates=[-1, 1], plot=False, debug=True)
     assert capsys.readouterr().out == "Objectives by k\nk: -1\n"
+
+
+def test_c_packer_equals_python_packer(llama_online_model):
+    """fleet_table (the C packer, distilp_amd/csrc/fleetpack.c) against fleet_table_py (the Python
+    restatement of the reference's field reads and truthiness tests): every field of 300 synthetic
+    fleets of 1..70 devices bit for bit, and the same exception type and message on bad input."""
+    import numpy as np
+
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, fleet_table_py
+    from distilp_amd.synth import synth_fleet
+
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(500 + s, 1 + (s * 7) % 70)] for s in range(300)]
+    a, b = fleet_table(fleets, llama_online_model), fleet_table_py(fleets, llama_online_model)
+    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS:
+        assert getattr(a, f).dtype == getattr(b, f).dtype and np.array_equal(getattr(a, f), getattr(b, f)), f
+
+    def err(fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001
+            return type(e), str(e)
+        return None
+
+    devs = fleets[5]
+    m = llama_online_model
+    cases = [
+        [devs, []],                                                           # empty fleet (kappa's IndexError)
+        [[devs[0].model_copy(update={"T_cpu": 0.0})] + devs[1:]],            # alpha: b' / T_cpu
+        [[d.model_copy(update={"s_disk": 0.0}) for d in devs]],              # kappa: s_disk
+        [[devs[0].model_copy(update={"scpu": {m.Q: {"b_2": 1.0}}})] + devs[1:]],  # b_1 missing
+        [[d.model_copy(update={"os_type": "android", "d_bytes_can_swap": 7, "d_swap_avail": 5}) for d in devs]],
+    ]
+    for fl in cases:
+        assert err(lambda: fleet_table(fl, m)) == err(lambda: fleet_table_py(fl, m)), fl
+    ok = fleet_table(cases[-1], m)
+    assert np.array_equal(ok.swap, fleet_table_py(cases[-1], m).swap) and (ok.swap == 5).all()
