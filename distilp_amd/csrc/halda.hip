@@ -168,8 +168,43 @@ extern "C" __device__ double __ockl_wfred_max_f64(double);
 extern "C" __device__ int __ockl_wfred_min_i32(int);
 extern "C" __device__ int __ockl_wfred_or_i32(int);
 extern "C" __device__ int __ockl_wfred_add_i32(int);
-__device__ inline double wave_min(double v) { return __ockl_wfred_min_f64(v); }
-__device__ inline double wave_max(double v) { return __ockl_wfred_max_f64(v); }
+// v_min_f64 / v_max_f64 as they are: for the non-signalling operands here they equal fmin / fmax
+// (a quiet NaN operand yields the other), without the canonicalising v_max_f64 x, x, x the compiler
+// puts in front of every fmin / fmax of a shuffled value.
+__device__ inline double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline double xor32_f64(double v, int lane);
+__device__ inline double xor16_f64(double v, int lane);
+template <int R>
+__device__ inline double ror16(double v);
+// min / max over the wave on every lane, without LDS or readlane: permlane swaps across the halves
+// and rows, then DPP row rotations (min and max are exact: any order gives the same value)
+__device__ inline double wave_min(double v) {
+    const int lane = int(__lane_id());
+    v = vmin_f64(v, xor32_f64(v, lane));
+    v = vmin_f64(v, xor16_f64(v, lane));
+    v = vmin_f64(v, ror16<8>(v));
+    v = vmin_f64(v, ror16<4>(v));
+    v = vmin_f64(v, ror16<2>(v));
+    return vmin_f64(v, ror16<1>(v));
+}
+__device__ inline double wave_max(double v) {
+    const int lane = int(__lane_id());
+    v = vmax_f64(v, xor32_f64(v, lane));
+    v = vmax_f64(v, xor16_f64(v, lane));
+    v = vmax_f64(v, ror16<8>(v));
+    v = vmax_f64(v, ror16<4>(v));
+    v = vmax_f64(v, ror16<2>(v));
+    return vmax_f64(v, ror16<1>(v));
+}
 __device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
 __device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
 __device__ inline int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
@@ -199,8 +234,8 @@ __device__ inline double xor_cross(double v, int lane) {
     const uint32_t hi = O == 32 ? xor32_u32(uint32_t(u >> 32), lane) : xor16_u32(uint32_t(u >> 32), lane);
     return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
 }
-template <int R>
-__device__ inline double ror16(double v);
+__device__ inline double xor32_f64(double v, int lane) { return xor_cross<32>(v, lane); }
+__device__ inline double xor16_f64(double v, int lane) { return xor_cross<16>(v, lane); }
 
 // Sum over the wave in the xor-butterfly order (steps 32, 16, 8, 4, 2, 1; every lane gets the same
 // bits). The cross-row steps are permlane swaps; after them a lane's value depends on its index
@@ -221,7 +256,7 @@ __device__ inline double wave_sum_f64(double v) {
 // Row rotation of a 16-lane DPP row (row_ror:R, R = 1..15): lane i reads lane (i + R) mod 16 of its row.
 template <int R>
 __device__ inline int ror16(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x120 + R, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, 0x120 + R, 0xf, 0xf, true);
 }
 template <int R>
 __device__ inline double ror16(double v) {
@@ -269,11 +304,11 @@ struct Seg {
     }
     __device__ inline double min_f64(double v) const {
         if constexpr (S_ == 64) return wave_min(v);
-        else return row16_reduce(v, [](double a, double b) { return fmin(a, b); });
+        else return row16_reduce(v, [](double a, double b) { return vmin_f64(a, b); });
     }
     __device__ inline double max_f64(double v) const {
         if constexpr (S_ == 64) return wave_max(v);
-        else return row16_reduce(v, [](double a, double b) { return fmax(a, b); });
+        else return row16_reduce(v, [](double a, double b) { return vmax_f64(a, b); });
     }
     __device__ inline double sum_f64(double v) const {
         if constexpr (S_ == 64) return wave_sum_f64(v);
@@ -1719,8 +1754,10 @@ struct FullRec {
 
 // Greedy exchange over lazily evaluated convex leaves (lane = device, M <= 64).
 // On K1_OK, e holds the device's extra layers.
+// gE / nE: the device's G(e) and its least minimiser n at the returned e -- split_full's values at
+// w = lb + e, so the caller's output needs no split of its own.
 template <class Rec, class SG>
-__device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int &rounds) {
+__device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int &rounds, double &gE, int &nE) {
     const int lane = sg.sl;  // device index within the problem
     const auto &d = rec.core();  // Dev, or the compact record with its specialised split
     const bool act = lane < M;
@@ -1730,12 +1767,15 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
     if (act) {
         const int wlo = rec_wlo(d), whi = rec_whi(d);
         ok0 = wlo <= whi && split_full(d, wlo, g0, n0, s);
-        ok1 = ok0 && wlo + 1 <= whi && split_step(d, wlo + 1, n0, g1, n1, s);
+        ok1 = ok0 && wlo + 1 <= whi && split_full(d, wlo + 1, g1, n1, s);
     }
     e = 0;
+    gE = g0;
+    nE = n0;
     // every leaf must start at e = 0 (a later start is legal but rare: general kernel)
-    if (sg.or_i(act && !ok0)) return K1_FALLBACK;
+    if (sg.bits(act && !ok0)) return K1_FALLBACK;
     double gn = ok1 ? g1 : kInf;               // G(e + 1)
+    int nN = n1;                               // its n
     double inc = ok1 ? g1 - g0 : kInf;        // G(e + 1) - G(e)
     double dprev = -kInf;                      // last taken increment (convexity check)
     int need = R;
@@ -1748,18 +1788,18 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         const double rv = act && lane != win ? inc : kInf;
         const double m2 = sg.min_f64(rv);
         const int d2 = sg.lowest(act && lane != win && rv == m2);
-        const int ew = sg.bcast(e, win);
+        const int ew = sg.bcast(e, win), nNw = sg.bcast(nN, win);
         const double gnw = sg.bcast(gn, win), dpw = sg.bcast(dprev, win);
         // the winner takes its next increment bv; lane t evaluates G_win(ew + 2 + t)
         int take = 1;
         bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
         double Gt = kInf, dt = kInf;
+        int nt = 0;
         if (need > 1) {
             const auto dw = rec.bcast(sg, win).core();
             const int wl = rec_wlo(dw) + ew + 2 + lane;
             double g = kInf;
-            int nn = 0;
-            if (wl <= rec_whi(dw) && split_full(dw, wl, g, nn, s)) Gt = g;
+            if (wl <= rec_whi(dw) && split_full(dw, wl, g, nt, s)) Gt = g;
             // shuffles on the full wave first (a bpermute under a lane-0-off mask would read 0 there)
             const double up = sg.up1(Gt);
             const double prev = lane == 0 ? gnw : up;
@@ -1777,11 +1817,16 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         if (bad) return K1_FALLBACK;
         // winner's new state: e = ew + take; G(e) and G(e + 1) from the evaluated window
         const double gcur = take == 1 ? gnw : sg.bcast(Gt, take - 2);
+        const int ncur = take == 1 ? nNw : sg.bcast(nt, take - 2);
         const double gnext = need > 1 ? sg.bcast(Gt, take - 1) : kInf;
+        const int nnext = need > 1 ? sg.bcast(nt, take - 1) : 0;
         const double tlast = take == 1 ? bv : sg.bcast(dt, take - 2);
         if (lane == win) {
             e = ew + take;
+            gE = gcur;
+            nE = ncur;
             gn = gnext;
+            nN = nnext;
             inc = gnext < kInf ? gnext - gcur : kInf;
             dprev = tlast;
         }
@@ -2145,8 +2190,9 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_PSTAMP(2);
     HALDA_PSTAMP(3);
     HALDA_PSTAMP(4);
-    int e = 0, rounds = 0;
-    const int rc = k1_alloc(FullRec{d}, I.M, I.W - sumlo, Wave(lane), e, rounds);
+    int e = 0, rounds = 0, nE = 0;
+    double gE = 0.0;
+    const int rc = k1_alloc(FullRec{d}, I.M, I.W - sumlo, Wave(lane), e, rounds, gE, nE);
     wave_sync();  // LDS records are rewritten by the next instance
     HALDA_PSTAMP(5);
     if (rc == K1_FALLBACK) {
@@ -2948,8 +2994,14 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, 
         dst = max(dst, int(kk));
     };
     if (r.cls == 1 || r.cls == 3 || (fl & HALDA_DEV_METAL_AVAIL)) K(rhs_ram(F, r.cls, c.bcio), r.Kset);
-    if (fl & HALDA_DEV_CUDA_OK) K(rhs_cuda(F), r.Kvram);
-    if (fl & HALDA_DEV_METAL_OK) K(rhs_metal(Mo, F), r.Kvram);
+    // VRAM rows: CUDA or Metal (one division for either; both rows only on a device with both)
+    const bool cu = fl & HALDA_DEV_CUDA_OK, mt = fl & HALDA_DEV_METAL_OK;
+    if (cu && mt) {
+        K(rhs_cuda(F), r.Kvram);
+        K(rhs_metal(Mo, F), r.Kvram);
+    } else if (cu || mt) {
+        K(cu ? rhs_cuda(F) : rhs_metal(Mo, F), r.Kvram);
+    }
     return r;
 }
 
@@ -3001,8 +3053,21 @@ __device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields
     const double tail = sg.sum_f64(act ? tail_term(mf) : 0.0);
     int hi = sg.lowest(act && (mf.flags & HALDA_DEV_HEAD));
     if (hi >= SG::S) hi = 0;
-    kappa = kappa_head(Mo, sg.bcast(mf.flags, hi), sg.bcast(mf.scpu, hi), sg.bcast(mf.Tc, hi), sg.bcast(mf.sdisk, hi)) +
-            tail;
+    // kappa_head's four quotients on lanes 0..3 of the problem (one division for the four), summed in
+    // its order
+    const int hf = sg.bcast(mf.flags, hi);
+    const double scpu = sg.bcast(mf.scpu, hi), Tc = sg.bcast(mf.Tc, hi), sdisk = sg.bcast(mf.sdisk, hi);
+    const double bv = Mo.b_in / Mo.V;
+    const int j = sg.sl & 3;
+    const double num = j == 0 ? Mo.f_out_b1 : j == 1 ? bv + Mo.b_out : j == 2 ? Mo.b_in : Mo.b_out;
+    const double den = j == 0 ? scpu : j == 1 ? Tc : j == 2 ? Mo.V * sdisk : sdisk;
+    const double q = num / den;
+    const double q0 = sg.bcast(q, 0), q1 = sg.bcast(q, 1), q2 = sg.bcast(q, 2), q3 = sg.bcast(q, 3);
+    double total = (Mo.has_f_out && (hf & HALDA_DEV_CPU_RATE)) ? (scpu > 0.0 ? 0.0 + q0 : 0.0) : 0.0;
+    total += q1;
+    total += q2;
+    total += q3;
+    kappa = total + tail;
 }
 
 __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
@@ -3162,7 +3227,9 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         bool improved = false;
         if (M == 0) st = W > 0 ? HALDA_STATUS_INFEASIBLE : HALDA_STATUS_OPTIMAL;  // x = [C = 0]
         else {
-            int rc = K1_FALLBACK, e = 0, rounds = 0;
+            int rc = K1_FALLBACK, e = 0, rounds = 0, nE = 0;
+            double gE = 0.0;
+            bool haveE = true;  // gE / nE hold the split at w = 1 + e (k1_alloc), else split here
             me.W = W;
             if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
             // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
@@ -3170,10 +3237,13 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M)) {
                 if constexpr (!kTables) {
                     // the register launch solves its greedy fallbacks itself (exact DP, R + 1 <= kDpLanes)
-                    if (!A.k1dp) rc = k1_alloc(me, M, W - M, sg, e, rounds);
-                    if (rc == K1_FALLBACK && W - M < kDpLanes) rc = k1_dp(me, M, W - M, sg, e, w.dparg);
+                    if (!A.k1dp) rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
+                    if (rc == K1_FALLBACK && W - M < kDpLanes) {
+                        rc = k1_dp(me, M, W - M, sg, e, w.dparg);
+                        haveE = false;
+                    }
                 } else {
-                    rc = k1_alloc(me, M, W - M, sg, e, rounds);
+                    rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
                 }
             }
             if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
@@ -3190,7 +3260,13 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 const int wl = 1 + e;
                 if (lane < M) {
                     double P, Q;
-                    split_full(me, wl, g, n, sl);
+                    if (haveE) {
+                        g = gE;
+                        n = nE;
+                        rec_slacks(me, wl, n, sl);
+                    } else {
+                        split_full(me, wl, g, n, sl);
+                    }
                     dev_cycle(me, wl, n, sl, P, Q);
                     z = Q > P ? 0.5 * (Q - P) : 0.0;
                     H = Q >= P ? 0.5 * (P + Q) : P;
