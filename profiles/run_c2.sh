@@ -6,7 +6,7 @@ R=${1:-r02}
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_${R}_c2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 300 python3 bench.py --M 16 --no-cpu-baseline --no-tto > "$OUT/c2_bench.json" 2> "$OUT/c2_bench.err"
+timeout -k 10 300 python3 bench.py --M 16 --no-cpu-baseline --no-tto --streams 1 > "$OUT/c2_bench.json" 2> "$OUT/c2_bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- \
     python3 tools/sweep_time.py --M 16,64 --iters 10 > "$OUT/trace.log" 2>&1
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
