@@ -236,7 +236,7 @@ def timed(step, steps, torch, dev, dist, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -344,6 +344,8 @@ def main():
     ap.add_argument("--streams", type=int, choices=(1, 2), default=2,
                     help="streams the k-sweep steps alternate over (1: every launch serialised, e.g. for "
                          "per-dispatch profiling)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
+    ap.add_argument("--share-gpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--M", type=int, default=64)
     ap.add_argument("--copies", type=int, default=0, help="resident copies per leg (0: enough to exceed the MALL)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -377,18 +379,23 @@ def main():
     import torch.distributed as dist
 
     n_dev = torch.cuda.device_count()
-    if n_dev < world or local >= n_dev:
+    if args.share_gpu:  # diagnostic: every rank on GPU 0 (exercises the multi-rank path on a 1-GPU box)
+        local = 0
+    elif n_dev < world or local >= n_dev:
         print(f"bench.py: --gpus {args.gpus} needs {world} GPUs on this node, {n_dev} visible", file=sys.stderr)
         return 2
     rccl_world = 1
+    torch.cuda.set_device(local)  # before the process group: its barriers run on this rank's GPU
+    dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group("gloo", init_method="env://")
         rccl_world = dist.get_world_size()
         if rccl_world != args.gpus:
             print(f"bench.py: RCCL world size {rccl_world} != --gpus {args.gpus}", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
     from distilp_amd.solver._libhalda import get_context
     from distilp_amd.solver.batch import assemble
