@@ -320,6 +320,31 @@ def time_to_optimal(model, M: int, runs: int = 100):
     return statistics.median(times)
 
 
+def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
+    """Config C5 (BASELINE.json configs[4]) end to end from the host: a base fleet (seed 0) re-profiled
+    per instance (every numeric device field x LU(0.9, 1.1), FleetTable.perturbed), batches of B
+    instances through halda_solve_fleets_host (PCIe in, the k-sweep, PCIe out), one at a time."""
+    from dataclasses import replace
+
+    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, solve_table
+
+    base = fleet_table(build_fleets([0], M), model)
+    big = replace(base, dev_off=np.arange(B + 1, dtype=np.int64) * M,
+                  **{f: np.tile(getattr(base, f), B) for f in ("os_class", "flags") + F64_FIELDS + I64_FIELDS})
+    rng = np.random.default_rng(10_000)
+    solve_table(big.perturbed(rng), model, KS_L80, 0.5)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(batches):
+        res = solve_table(big.perturbed(rng), model, KS_L80, 0.5)
+        if not (res.best_k > 0).all():
+            raise RuntimeError("C5: a re-profiled fleet without a feasible k")
+    dt = (time.perf_counter() - t0) / batches
+    return {"what": f"C5: re-profiled M={M} fleet, batches of {B} perturbed instances (host perturbation, PCIe in, "
+                    "k-sweep, PCIe out; synchronous, one batch at a time)",
+            "ms_per_batch": dt * 1e3, "fleets_per_s": B / dt, "instances_per_s": B * len(KS_L80) / dt,
+            "target_instances_per_s": 10_000}
+
+
 def launch_ranks(args) -> int:
     """--gpus N from a plain `python bench.py`: start N ranks (one process per GPU) with
     torch.distributed.run before this process touches the GPU, relay their output and exit code."""
@@ -500,6 +525,7 @@ def main():
     n_fleets_total = (len(fleets) * world if not strong_head else C3_FLEETS) * args.steps
     if rank == 0:
         tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
+        c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -543,6 +569,7 @@ def main():
                 "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,
                 "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
             },
+            "c5_stream": c5,
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,
         }
