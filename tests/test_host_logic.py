@@ -179,3 +179,19 @@ def test_c_packer_equals_python_packer(llama_online_model):
         assert err(lambda: fleet_table(fl, m)) == err(lambda: fleet_table_py(fl, m)), fl
     ok = fleet_table(cases[-1], m)
     assert np.array_equal(ok.swap, fleet_table_py(cases[-1], m).swap) and (ok.swap == 5).all()
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    """`bench.py --gpus 2` inside a one-rank launch exits with an error (before any GPU call), instead
+    of reporting n_gpus: 1."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 2 and "--gpus 2 but the launcher started 1 rank" in p.stderr
+    assert p.stdout.strip() == ""
