@@ -3089,6 +3089,21 @@ __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fle
     kappa = kappa_head(Mo, F.flags[h], F.scpu_b1[h], F.T_cpu[h], F.s_disk[h]) + tail;
 }
 
+// A uniform read of read-only memory through the scalar cache (s_load): the constant address space
+// tells the compiler the value cannot change under the kernel (a plain global read of a uniform
+// address is a vector load, a full memory round trip before the loads that depend on it).
+__device__ inline int64_t sload_i64(const int64_t *p) {
+    return *reinterpret_cast<const __attribute__((address_space(4))) int64_t *>(
+        reinterpret_cast<uintptr_t>(p));
+}
+
+// No instruction: the record's registers are redefined for the optimiser (stops loop-invariant
+// hoisting of values derived from it).
+__device__ inline void opaque_rec(FieldRec &r) {
+    asm volatile("" : "+v"(r.alpha), "+v"(r.b), "+v"(r.p_bp), "+v"(r.p_b), "+v"(r.cst), "+v"(r.Kset), "+v"(r.Kvram),
+                 "+v"(r.cls), "+v"(r.gpu));
+}
+
 struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
@@ -3155,9 +3170,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     const bool kl = lane < A.n_k;
     const int kj = A.ks[kl ? lane : 0];
     const int Wj = kl ? A.Ws[lane] : 0;
-    // the fleet's extent: with one fleet size for the batch, from the (uniform, scalar-cached)
-    // dev_off[0], so that the field loads are the wave's first vector round trip
-    const int64_t d0 = A.uM > 0 ? F.dev_off[0] + int64_t(f) * A.uM : F.dev_off[f];
+    // the fleet's extent: with one fleet size for the batch, from dev_off[0] read through the scalar
+    // cache (the table is read-only to the kernel), so that the field loads are the wave's first
+    // vector round trip
+    const int64_t d0 = A.uM > 0 ? sload_i64(F.dev_off) + int64_t(f) * A.uM : F.dev_off[f];
     const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
     bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
     if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
@@ -3167,6 +3183,12 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     if (regs) {
         // every field of this lane's device in one round trip (lanes past M read device 0)
         const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+#if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 3  // diagnostic build only: the field loads alone
+        if (lane < M)
+            A.out.n[d0 + lane] = int(mf.scpu + mf.sgpu + mf.Tc + mf.Tg + mf.tkc + mf.tkg + mf.r2v + mf.v2r + mf.tcomm +
+                                     mf.sdisk) + int(mf.ram + mf.ccpu + mf.cgpu + mf.cuda + mf.metal + mf.swap) + mf.cls + mf.flags;
+        return;
+#endif
         me = field_rec(Mo, mf, bad);
         bad = lane < M ? bad : 0;
         if (M > 0) fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
@@ -3215,9 +3237,16 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         }
     }
     uint64_t todo = sg.bits(kl && stj == kOpen);
+    const int M_all = M;
     while (todo) {
         const int j = __builtin_ctzll(todo);
         todo &= todo - 1;
+        // the record and M are opaque to the compiler at each k: nothing derived from them is hoisted
+        // out of this loop (hoisted per-lane masks and addresses held across the loop spill SGPRs; most
+        // fleets open one k)
+        opaque_rec(me);
+        int M = M_all;
+        if constexpr (!kSeg) asm volatile("" : "+s"(M));
         const int k = sg.bcast(kj, j);
         const int W = sg.bcast(Wj, j);
         const int64_t inst = int64_t(f) * A.n_k + j;
