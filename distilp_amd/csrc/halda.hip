@@ -2885,29 +2885,28 @@ __device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) 
     const int nhi = r.gpu ? r.W : 0;
     nL = r.cls == 3 && hs ? max(0, w + r.Kset - r.W) : 0;
     nU = min(nhi, w);
-    if (r.Kvram != kNoRow) nU = min(nU, nhi - r.Kvram);
+    nU = r.Kvram != kNoRow ? min(nU, nhi - r.Kvram) : nU;
     const bool setok = !(hs && (r.cls == 1 || r.cls == 2)) || max(0, w + r.Kset) <= r.W;
     return nL <= nU && setok;
 }
 
-// dev_cost on dev() for (w, n) and the least slacks (sc = the class slack, t = VRAM).
-__device__ inline double rec_cost(const FieldRec &r, int w, int n, int sc, int t) {
-    const double pv = rec_pv(r);
-    double g = r.alpha * double(w);
-    g = g + r.b * double(n);
-    if (rec_own(r)) g = g + pv * double(sc);
-    g = g + pv * double(t);
-    return rec_nanx(r) ? __builtin_nan("") : g;
-}
-
-__device__ inline void rec_try(const FieldRec &r, int w, int nn, int nL, int nU, double &best, int &bn) {
+// One candidate n of a split, branch-free (selects, non-short-circuit tests): dev_cost on dev() for
+// (w, n) and its least slacks (sc = the class slack, t = VRAM), in dev_cost's term order (aw = alpha
+// w, pv = rec_pv, own = rec_own), and the tie rule "smaller cost, then smaller n". The record's NaN
+// flag (rec_nanx) is applied by the caller: it fails the whole split, as a NaN cost at every
+// candidate does.
+__device__ inline void rec_try(const FieldRec &r, double aw, double pv, bool own, int w, int nn, int nL, int nU,
+                               double &best, int &bn) {
     nn = min(max(nn, nL), nU);
     const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
-    const double g = rec_cost(r, w, nn, sc, t);
-    if (g < best || (g == best && nn < bn)) {
-        best = g;
-        bn = nn;
-    }
+    double g = aw;
+    g = g + r.b * double(nn);
+    const double gs = g + pv * double(sc);
+    g = own ? gs : g;
+    g = g + pv * double(t);
+    const bool better = (g < best) | ((g == best) & (nn < bn));
+    best = better ? g : best;
+    bn = better ? nn : bn;
 }
 
 __device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
@@ -2918,34 +2917,46 @@ __device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
     s[3] = max(0, n + r.Kvram);
 }
 
+// split_full on dev(): candidates nL, nU, the class-slack kink (class 3) and the VRAM kink, in that
+// order. Every candidate is evaluated on every lane (no divergent branches); an absent kink re-tries
+// nL, which never changes (best, bn): after nL's own try either bn = nL or best < cost(nL), and no
+// candidate lies below nL.
 __device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
     int nL, nU;
-    if (!rec_interval(r, w, nL, nU)) return false;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
     double best = kInf;
     int bn = -1;
-    rec_try(r, w, nL, nL, nU, best, bn);
-    rec_try(r, w, nU, nL, nU, best, bn);
-    if (r.cls == 3 && r.Kset != kNoRow) rec_try(r, w, w + r.Kset, nL, nU, best, bn);  // class-slack kink
-    if (r.Kvram != kNoRow) rec_try(r, w, -r.Kvram, nL, nU, best, bn);                  // VRAM kink
-    if (bn < 0) return false;
-    g = best;
-    n = bn;
-    rec_slacks(r, w, bn, s);
-    return true;
+    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, r.cls == 3 && r.Kset != kNoRow ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
+    rec_try(r, aw, pv, own, w, r.Kvram != kNoRow ? -r.Kvram : nL, nL, nU, best, bn);                  // VRAM kink
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
 }
 
 __device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &g, int &n, int s[4]) {
     int nL, nU;
-    if (!rec_interval(r, w, nL, nU)) return false;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
     double best = kInf;
     int bn = -1;
-    rec_try(r, w, n_prev, nL, nU, best, bn);
-    rec_try(r, w, n_prev + 1, nL, nU, best, bn);
-    if (bn < 0) return false;
-    g = best;
-    n = bn;
-    rec_slacks(r, w, bn, s);
-    return true;
+    rec_try(r, aw, pv, own, w, n_prev, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, n_prev + 1, nL, nU, best, bn);
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
 }
 
 // dev_cycle on dev(): rows (alpha, alpha + p_bp) w + b n + slack terms <= -cst.
@@ -2955,9 +2966,14 @@ __device__ inline void dev_cycle(const FieldRec &r, int w, int n, const int s[4]
     const double t0 = r.b * double(n), tc = pv * double(sc), tv = pv * double(s[3]);
     double a1 = r.alpha * double(w), a2 = (r.alpha + r.p_bp) * double(w);
     a1 = a1 + t0; a2 = a2 + t0;
-    if (rec_own(r)) { a1 = a1 + tc; a2 = a2 + tc; }
+    const bool own = rec_own(r);
+    const double o1 = a1 + tc, o2 = a2 + tc;
+    a1 = own ? o1 : a1;
+    a2 = own ? o2 : a2;
     a1 = a1 + tv; a2 = a2 + tv;
-    if (rec_nanx(r)) a1 = a2 = __builtin_nan("");
+    const bool nanx = rec_nanx(r);
+    a1 = nanx ? __builtin_nan("") : a1;
+    a2 = nanx ? __builtin_nan("") : a2;
     P = a1 - (-r.cst);
     Q = a2 - (-r.cst);
 }
