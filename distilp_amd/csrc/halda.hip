@@ -571,15 +571,14 @@ __device__ inline void n_interval(const Dev &d, int w, int &nL, int &nU) {
 __device__ inline void try_split(const Dev &d, int w, int nn, int nL, int nU, double &best, int &bn, int bs[4]) {
     nn = min(max(nn, nL), nU);
     int s[4];
-    if (least_slacks(d, w, nn, s)) {
-        const double g = dev_cost(d, w, nn, s);
-        if (g < best || (g == best && nn < bn)) {
-            best = g;
-            bn = nn;
+    const bool ok = least_slacks(d, w, nn, s);
+    const double g = dev_cost(d, w, nn, s);
+    // branch-free: selects and non-short-circuit tests (the same update as "if ok and better")
+    const bool better = ok & ((g < best) | ((g == best) & (nn < bn)));
+    best = better ? g : best;
+    bn = better ? nn : bn;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bs[j] = s[j];
-        }
-    }
+    for (int j = 0; j < 4; ++j) bs[j] = better ? s[j] : bs[j];
 }
 
 // Best GPU split n for w layers by full candidate search. The cost is convex
@@ -2852,18 +2851,28 @@ struct FieldRec {
         return o;
     }
     template <class SG>
-    __device__ inline FieldRec bcast(const SG &sg, int src) const {  // the problem's device src, on every lane
-        FieldRec o;
-        o.alpha = sg.bcast(alpha, src); o.b = sg.bcast(b, src); o.p_bp = sg.bcast(p_bp, src);
-        o.p_b = sg.bcast(p_b, src); o.cst = sg.bcast(cst, src);
-        o.Kset = sg.bcast(Kset, src); o.Kvram = sg.bcast(Kvram, src);
-        const int cg = sg.bcast(cls | (gpu << 4), src);
-        o.cls = cg & 15; o.gpu = cg >> 4;
-        o.W = W;
-        return o;
-    }
+    __device__ inline auto bcast(const SG &sg, int src) const;  // the problem's device src, on every lane
     __device__ inline const FieldRec &core() const { return *this; }
 };
+
+// A record broadcast to the whole problem (every lane holds device src's record): its split takes
+// the branches on the record's shape instead of selects (they are uniform here), skipping the
+// candidates the device does not have; the same candidates, order and tie rule as on a FieldRec.
+struct UFieldRec : FieldRec {
+    __device__ inline const UFieldRec &core() const { return *this; }
+};
+
+template <class SG>
+__device__ inline auto FieldRec::bcast(const SG &sg, int src) const {
+    UFieldRec o;
+    o.alpha = sg.bcast(alpha, src); o.b = sg.bcast(b, src); o.p_bp = sg.bcast(p_bp, src);
+    o.p_b = sg.bcast(p_b, src); o.cst = sg.bcast(cst, src);
+    o.Kset = sg.bcast(Kset, src); o.Kvram = sg.bcast(Kvram, src);
+    const int cg = sg.bcast(cls | (gpu << 4), src);
+    o.cls = cg & 15; o.gpu = cg >> 4;
+    o.W = W;
+    return o;
+}
 
 // The solve primitives on a FieldRec, specialised. The Dev that dev() expands a record to has two
 // live slacks: its class slack s_c >= w + Kset (class 3: w - n + Kset; s_c <= W) and the VRAM slack
@@ -2921,7 +2930,8 @@ __device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
 // order. Every candidate is evaluated on every lane (no divergent branches); an absent kink re-tries
 // nL, which never changes (best, bn): after nL's own try either bn = nL or best < cost(nL), and no
 // candidate lies below nL.
-__device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+template <bool kUniform>
+__device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int &n, int s[4]) {
     int nL, nU;
     const bool okI = rec_interval(r, w, nL, nU);
     const double pv = rec_pv(r), aw = r.alpha * double(w);
@@ -2930,8 +2940,9 @@ __device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, i
     int bn = -1;
     rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
     rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, r.cls == 3 && r.Kset != kNoRow ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
-    rec_try(r, aw, pv, own, w, r.Kvram != kNoRow ? -r.Kvram : nL, nL, nU, best, bn);                  // VRAM kink
+    const bool hc = r.cls == 3 && r.Kset != kNoRow, hv = r.Kvram != kNoRow;
+    if (!kUniform || hc) rec_try(r, aw, pv, own, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
+    if (!kUniform || hv) rec_try(r, aw, pv, own, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
@@ -2939,6 +2950,12 @@ __device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, i
         rec_slacks(r, w, bn, s);
     }
     return ok;
+}
+__device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    return split_full_impl<false>(r, w, g, n, s);
+}
+__device__ inline bool split_full(const UFieldRec &r, int w, double &g, int &n, int s[4]) {
+    return split_full_impl<true>(r, w, g, n, s);
 }
 
 __device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &g, int &n, int s[4]) {
