@@ -48,6 +48,14 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# The sweep kernel is bound by FP64 VALU issue, not HBM: its VALU roof beside the HBM one.
+# VALU instructions per wave of halda_sweep_kernel on the C3 workload (one wave = one M = 64 fleet):
+# SQ_INSTS_VALU / SQ_WAVES from rocprofv3 (profiles/r02_sq_counters.txt); a wave64 VALU instruction holds
+# its SIMD for >= 4 cycles (FP64 add / mul / FMA issue at full rate), 1,024 SIMDs at <= 2.4 GHz.
+SWEEP_VALU_PER_WAVE = 1259
+VALU_CYCLES = 4
+N_SIMDS = 1024
+CLOCK_GHZ = 2.4
 KS_L80 = [1, 2, 4, 5, 8, 10, 16, 20, 40]
 METRIC = "HALDA MILP instances solved/sec (node), M=64 devs L=80; time-to-optimal"
 C3_FLEETS = 4096
@@ -578,6 +586,14 @@ def main():
             # the same bytes over the pipelined step time (two streams: batches overlap on the device)
             a = rf["algorithmic_bytes_per_launch"] / (line["ms_per_step"] * 1e-3) / 1e9
             rf["pipelined"] = {"achieved": a, "frac": a / HBM_PEAK_GBS, "ms_per_step": line["ms_per_step"]}
+            if rf["kernel"] == "halda_sweep_kernel" and args.M == 64 and ks == KS_L80:
+                need = len(fleets) * SWEEP_VALU_PER_WAVE * VALU_CYCLES / (N_SIMDS * CLOCK_GHZ * 1e9)
+                rf["valu_issue"] = {
+                    "what": "FP64-VALU-issue roof of the same launch: VALU cycles its waves need / SIMD cycles "
+                            "in the launch time (profiled VALU count, peak clock)",
+                    "valu_per_wave": SWEEP_VALU_PER_WAVE, "waves": len(fleets), "cycles_per_valu": VALU_CYCLES,
+                    "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": "profiles/r02_sq_counters.txt",
+                    "frac": need / (rf["kernel_ms"] * 1e-3), "frac_pipelined": need / (line["ms_per_step"] * 1e-3)}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
