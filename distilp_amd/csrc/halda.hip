@@ -3137,23 +3137,26 @@ __device__ inline void opaque_rec(FieldRec &r) {
                  "+v"(r.cls), "+v"(r.gpu));
 }
 
+// Kernel arguments. Everything a wave reads through the scalar cache comes first (six 64-B lines:
+// the model, the table pointers, the result pointers, the counts); the k list, which lanes read
+// with vector loads, last.
 struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
-    int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
-    int32_t Ws[64];  // W = L / k per k (host integer division)
     int n_k;
+    int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
     halda_fleet_result out;
     int64_t xstride;
     uint8_t *fflag;  // per fleet: 1 = needs the table launch
     int *hb_flag;
     int launch_id;
+    int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
+    int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
     int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
     unsigned char *gtab;           // kGlobal: per-wave slices
     int64_t gstride;
-    int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
-    int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
-    int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
+    int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
+    int32_t Ws[64];  // W = L / k per k (host integer division)
 };
 
 // x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
@@ -3206,7 +3209,9 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     // the fleet's extent: with one fleet size for the batch, from dev_off[0] read through the scalar
     // cache (the table is read-only to the kernel), so that the field loads are the wave's first
     // vector round trip
-    const int64_t d0 = A.uM > 0 ? sload_i64(F.dev_off) + int64_t(f) * A.uM : F.dev_off[f];
+    // with one fleet size for the batch the first device is dev_off[0] + f uM; dev_off[0] (0 in the
+    // usual table) is read beside the field loads below, not in front of them
+    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM : F.dev_off[f];
     const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
     bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
     if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
@@ -3214,8 +3219,21 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     int bad = 0;
     double tsum = 0.0, xsum = 0.0, kappa = 0.0;
     if (regs) {
-        // every field of this lane's device in one round trip (lanes past M read device 0)
-        const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        // every field of this lane's device in one round trip (lanes past M read device 0). With one
+        // fleet size the loads are issued at once from dev_off[0] = 0 (the usual table) while the
+        // scalar read of dev_off[0] is in flight, and reissued only where it is not 0: no dependent
+        // round trip in front of the field loads.
+        DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        if (A.uM > 0) {
+            // a vector read (returns in order behind the field loads: no wait of its own, unlike a
+            // scalar read, whose lgkmcnt wait would also hold the kernel-argument reads)
+            const int64_t base = __builtin_amdgcn_readfirstlane(int(F.dev_off[0])) |
+                                 (int64_t(__builtin_amdgcn_readfirstlane(int(uint64_t(F.dev_off[0]) >> 32))) << 32);
+            if (base != 0) {
+                d0 += base;
+                mf = load_fields(F, d0 + (lane < M ? lane : 0));
+            }
+        }
 #if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 3  // diagnostic build only: the field loads alone
         if (lane < M)
             A.out.n[d0 + lane] = int(mf.scpu + mf.sgpu + mf.Tc + mf.Tg + mf.tkc + mf.tkg + mf.r2v + mf.v2r + mf.tcomm +
@@ -3226,6 +3244,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         bad = lane < M ? bad : 0;
         if (M > 0) fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
     } else {
+        if (A.uM > 0) d0 += sload_i64(F.dev_off);
         for (int i = lane; i < M; i += 64) {
             int b1 = 0;
             field_rec(Mo, load_fields(F, d0 + i), b1);
@@ -3294,6 +3313,11 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             bool haveE = true;  // gE / nE hold the split at w = 1 + e (k1_alloc), else split here
             me.W = W;
             if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 4  // diagnostic build only: stop before the first greedy
+            if (lane < M) A.out.n[d0 + lane] = me.Kset + me.Kvram + int(me.alpha + me.b + me.p_bp + me.p_b + me.cst) + W + k;
+            if (lane == 0) A.out.obj_value[f] = tsum + xsum + kappa;
+            return;
+#endif
             // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
             // the solution for any k (the output adds (k - 1) max_i H_i)
             if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M)) {
@@ -3531,6 +3555,18 @@ constexpr int kSweepWavesPerBlock = 4;  // fleets per workgroup of the register-
 __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_kernel(SweepArgs A) {
     // wave-uniform by construction; readfirstlane lets the compiler know (scalar fleet addressing)
     const int f = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    {
+        // the kernel arguments the first branches read, fetched together with one value of every other
+        // 64-B line of SweepArgs the wave reads through the scalar cache (the model, the table and
+        // result pointers): one round trip instead of one per branch and line (each lgkmcnt wait would
+        // otherwise hold the next read back)
+        const int nf = A.F.n_fleets, nk = A.n_k, um = A.uM;
+        const int64_t *doff = A.F.dev_off;
+        const double bp = A.Mo.b_prime;
+        const double *tc = A.F.T_cpu;
+        const int32_t *ow = A.out.w;
+        asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
+    }
     if (f >= A.F.n_fleets) return;
 #ifdef HALDA_SWEEP_STAGGER
     {  // experiment: the waves sharing a SIMD start their loads one after another (slot = HW wave id)
