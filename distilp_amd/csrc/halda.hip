@@ -1764,9 +1764,18 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
     int n0 = 0, n1 = 0, s[4];
     bool ok0 = false, ok1 = false;
     if (act) {
+        // both splits evaluated unconditionally (independent: they interleave), used only where valid
         const int wlo = rec_wlo(d), whi = rec_whi(d);
-        ok0 = wlo <= whi && split_full(d, wlo, g0, n0, s);
-        ok1 = ok0 && wlo + 1 <= whi && split_full(d, wlo + 1, g1, n1, s);
+        double ga, gb;
+        int na, nb, sb[4];
+        const bool fa = split_full(d, wlo, ga, na, s);
+        const bool fb = split_full(d, wlo + 1, gb, nb, sb);
+        ok0 = wlo <= whi && fa;
+        ok1 = ok0 && wlo + 1 <= whi && fb;
+        g0 = ok0 ? ga : g0;
+        n0 = ok0 ? na : n0;
+        g1 = ok1 ? gb : g1;
+        n1 = ok1 ? nb : n1;
     }
     e = 0;
     gE = g0;
