@@ -3557,7 +3557,10 @@ __device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base)
 #ifndef HALDA_SWEEP_WAVES_PER_SIMD
 #define HALDA_SWEEP_WAVES_PER_SIMD 4  // occupancy target of the register-only sweep (as the k = 1 kernel)
 #endif
-constexpr int kSweepWavesPerBlock = 4;  // fleets per workgroup of the register-only sweep
+#ifndef HALDA_SWEEP_WPB
+#define HALDA_SWEEP_WPB 4
+#endif
+constexpr int kSweepWavesPerBlock = HALDA_SWEEP_WPB;  // fleets per workgroup of the register-only sweep
 
 // The register-only sweep: exactly one fleet per wave, kSweepWavesPerBlock waves per workgroup (a
 // quarter of the workgroups to dispatch); no loop, so no kernel argument stays live past its use.
@@ -3577,6 +3580,10 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
         asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
     }
     if (f >= A.F.n_fleets) return;
+#if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 5  // diagnostic build only: the launch alone
+    if ((threadIdx.x & 63) == 0) A.out.best_k[f] = 0;
+    return;
+#endif
 #ifdef HALDA_SWEEP_STAGGER
     {  // experiment: the waves sharing a SIMD start their loads one after another (slot = HW wave id)
         const int slot = __builtin_amdgcn_s_getreg(4 | (3 << 11)) & 3;
