@@ -181,29 +181,40 @@ __device__ inline double vmax_f64(double a, double b) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-__device__ inline double xor32_f64(double v, int lane);
-__device__ inline double xor16_f64(double v, int lane);
 template <int R>
 __device__ inline double ror16(double v);
 // min / max over the wave on every lane, without LDS or readlane: permlane swaps across the halves
 // and rows, then DPP row rotations (min and max are exact: any order gives the same value)
+// GFX9 DPP row broadcasts of a double (rows outside row_mask keep `old`): row_bcast:15 (0x142) gives
+// rows 1 / 3 lane 15 / 47, row_bcast:31 (0x143) gives rows 2 / 3 lane 31.
+template <int Ctrl, int RowMask>
+__device__ inline double dpp_bcast_f64(double old, double v) {
+    const uint64_t o = __builtin_bit_cast(uint64_t, old), u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = uint32_t(__builtin_amdgcn_update_dpp(int(uint32_t(o)), int(uint32_t(u)), Ctrl, RowMask, 0xf, false));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_update_dpp(int(uint32_t(o >> 32)), int(uint32_t(u >> 32)), Ctrl, RowMask, 0xf, false));
+    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+__device__ inline double bcast(double v, int src);
+// min / max over the wave, uniform: every row reduced by DPP rotations, the rows combined by the
+// row broadcasts (lane 63 ends up with all four), read from lane 63 (min and max are exact: any
+// order gives the same value). Every lane must be active.
 __device__ inline double wave_min(double v) {
-    const int lane = int(__lane_id());
-    v = vmin_f64(v, xor32_f64(v, lane));
-    v = vmin_f64(v, xor16_f64(v, lane));
     v = vmin_f64(v, ror16<8>(v));
     v = vmin_f64(v, ror16<4>(v));
     v = vmin_f64(v, ror16<2>(v));
-    return vmin_f64(v, ror16<1>(v));
+    v = vmin_f64(v, ror16<1>(v));
+    v = vmin_f64(v, dpp_bcast_f64<0x142, 0xa>(v, v));
+    v = vmin_f64(v, dpp_bcast_f64<0x143, 0xc>(v, v));
+    return bcast(v, 63);
 }
 __device__ inline double wave_max(double v) {
-    const int lane = int(__lane_id());
-    v = vmax_f64(v, xor32_f64(v, lane));
-    v = vmax_f64(v, xor16_f64(v, lane));
     v = vmax_f64(v, ror16<8>(v));
     v = vmax_f64(v, ror16<4>(v));
     v = vmax_f64(v, ror16<2>(v));
-    return vmax_f64(v, ror16<1>(v));
+    v = vmax_f64(v, ror16<1>(v));
+    v = vmax_f64(v, dpp_bcast_f64<0x142, 0xa>(v, v));
+    v = vmax_f64(v, dpp_bcast_f64<0x143, 0xc>(v, v));
+    return bcast(v, 63);
 }
 __device__ inline int wave_imin(int v) { return __ockl_wfred_min_i32(v); }
 __device__ inline int wave_or(int v) { return __ockl_wfred_or_i32(v); }
@@ -234,8 +245,6 @@ __device__ inline double xor_cross(double v, int lane) {
     const uint32_t hi = O == 32 ? xor32_u32(uint32_t(u >> 32), lane) : xor16_u32(uint32_t(u >> 32), lane);
     return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
 }
-__device__ inline double xor32_f64(double v, int lane) { return xor_cross<32>(v, lane); }
-__device__ inline double xor16_f64(double v, int lane) { return xor_cross<16>(v, lane); }
 
 // Sum over the wave in the xor-butterfly order (steps 32, 16, 8, 4, 2, 1; every lane gets the same
 // bits). The cross-row steps are permlane swaps; after them a lane's value depends on its index
