@@ -228,38 +228,19 @@ __device__ inline double bcast(double v, int src) {
 }
 __device__ inline int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 
-// v of lane i ^ 32 / i ^ 16 without LDS (gfx950 permlane swaps: a copy's upper half / odd rows
-// exchanged with the other copy's lower half / even rows).
-__device__ inline uint32_t xor32_u32(uint32_t v, int lane) {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, true, false);
-    return (lane & 32) ? r[0] : r[1];
-}
-__device__ inline uint32_t xor16_u32(uint32_t v, int lane) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, true, false);
-    return (lane & 16) ? r[0] : r[1];
-}
-template <int O>
-__device__ inline double xor_cross(double v, int lane) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = O == 32 ? xor32_u32(uint32_t(u), lane) : xor16_u32(uint32_t(u), lane);
-    const uint32_t hi = O == 32 ? xor32_u32(uint32_t(u >> 32), lane) : xor16_u32(uint32_t(u >> 32), lane);
-    return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-}
-
-// Sum over the wave in the xor-butterfly order (steps 32, 16, 8, 4, 2, 1; every lane gets the same
-// bits). The cross-row steps are permlane swaps; after them a lane's value depends on its index
-// mod 16 only, so the in-row steps are DPP row rotations by 8, 4, 2, 1, whose partner holds the xor
-// partner's value (see row16_reduce): the same operands in the same order as shuffles through
-// LDS, without the LDS round trips. Every lane must be active.
+// Sum over the wave in a fixed order, uniform: each 16-lane row all-reduced by DPP row rotations by
+// 8, 4, 2, 1 (row16_reduce's steps: every lane of a row holds its row sum S_r), then
+// (S3 + S2) + (S1 + S0) by the GFX9 row broadcasts, read from lane 63. With data in row 0 only (a
+// problem of <= 16 devices) the result is S0 exactly, the bits of row16_reduce (Seg<16>). Every lane
+// must be active.
 __device__ inline double wave_sum_f64(double v) {
-    const int lane = int(__lane_id());
-    v = v + xor_cross<32>(v, lane);
-    v = v + xor_cross<16>(v, lane);
     v = v + ror16<8>(v);
     v = v + ror16<4>(v);
     v = v + ror16<2>(v);
     v = v + ror16<1>(v);
-    return v;
+    v = v + dpp_bcast_f64<0x142, 0xa>(v, v);  // rows 1 / 3: S1 + S0, S3 + S2 (rows 0 / 2 unused)
+    v = v + dpp_bcast_f64<0x143, 0xc>(v, v);  // row 3: (S3 + S2) + (S1 + S0)
+    return bcast(v, 63);
 }
 
 // Row rotation of a 16-lane DPP row (row_ror:R, R = 1..15): lane i reads lane (i + R) mod 16 of its row.
