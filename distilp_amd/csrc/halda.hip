@@ -308,6 +308,7 @@ struct Seg {
         if constexpr (S_ == 64) return wave_sum(v);
         else return row16_reduce(v, [](int a, int b) { return a + b; });
     }
+    __device__ inline bool any(bool p) const { return bits(p) != 0; }  // a ballot, no reduction
     __device__ inline int or_i(int v) const {
         if constexpr (S_ == 64) return wave_or(v);
         else return row16_reduce(v, [](int a, int b) { return a | b; });
@@ -1408,8 +1409,8 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
                 ++cnt;
             }
         }
-    if (sg.or_i(act && (!ok || !mono))) return -1;
-    if (sg.or_i(act && cnt == 0)) return 0;
+    if (sg.any(act && (!ok || !mono))) return -1;
+    if (sg.any(act && cnt == 0)) return 0;
     LeafInfo li;
     li.convex = true;
     li.mono = true;
@@ -3251,7 +3252,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         }
         fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
     }
-    bad = sg.or_i(bad);
+    bad = sg.any(bad != 0) ? 1 : 0;
     HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(9, __builtin_amdgcn_s_memrealtime());
 #if defined(HALDA_DIAG_EXIT) && HALDA_DIAG_EXIT == 1  // diagnostic build only: stop after the records
