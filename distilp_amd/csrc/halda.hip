@@ -593,6 +593,8 @@ __device__ inline bool split_full(const Dev &d, int w, double &g, int &n, int s[
     return true;
 }
 
+__device__ inline bool split_first(const Dev &d, int w, double &g, int &n, int s[4]) { return split_full(d, w, g, n, s); }
+
 // Incremental step w-1 -> w. The cost is L-natural convex in (w, n) (every term
 // depends on w, n or w - n only; validated at decode), so the least minimiser
 // moves by 0 or +1: only n_prev and n_prev + 1 are candidates.
@@ -1759,7 +1761,7 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         const int wlo = rec_wlo(d), whi = rec_whi(d);
         double ga, gb;
         int na, nb, sb[4];
-        const bool fa = split_full(d, wlo, ga, na, s);
+        const bool fa = split_first(d, wlo, ga, na, s);
         const bool fb = split_full(d, wlo + 1, gb, nb, sb);
         ok0 = wlo <= whi && fa;
         ok1 = ok0 && wlo + 1 <= whi && fb;
@@ -2953,6 +2955,27 @@ __device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int 
 }
 __device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
     return split_full_impl<false>(r, w, g, n, s);
+}
+// split_full at w = 1 (the record's lower bound): 0 <= nL <= n <= nU <= w = 1, so every kink clamps
+// to nL or nU and re-trying either is a no-op (after nU's try best <= cost(nU), and on a tie bn <= nU):
+// the two end tries give split_full's result.
+__device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    if (w != 1) return split_full(r, w, g, n, s);
+    int nL, nU;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
 }
 __device__ inline bool split_full(const UFieldRec &r, int w, double &g, int &n, int s[4]) {
     return split_full_impl<true>(r, w, g, n, s);
