@@ -3367,8 +3367,11 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 double g = 0.0, H = 0.0, z = 0.0;
                 int n = 0, sl[4] = {0, 0, 0, 0};
                 const int wl = 1 + e;
+                // the cycle times only matter through (k - 1) max H and the x output: at k = 1 without x
+                // the largest cycle time is not formed (kc * hmax is +0 either way: hmax is finite and
+                // >= 0 after a successful split)
+                const bool need_h = kc != 0.0 || A.out.x;
                 if (lane < M) {
-                    double P, Q;
                     if (haveE) {
                         g = gE;
                         n = nE;
@@ -3376,11 +3379,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                     } else {
                         split_full(me, wl, g, n, sl);
                     }
-                    dev_cycle(me, wl, n, sl, P, Q);
-                    z = Q > P ? 0.5 * (Q - P) : 0.0;
-                    H = Q >= P ? 0.5 * (P + Q) : P;
+                    if (need_h) {
+                        double P, Q;
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        z = Q > P ? 0.5 * (Q - P) : 0.0;
+                        H = Q >= P ? 0.5 * (P + Q) : P;
+                    }
                 }
-                const double hmax = fmax(0.0, sg.max_f64(lane < M ? H : 0.0));
+                const double hmax = need_h ? fmax(0.0, sg.max_f64(lane < M ? H : 0.0)) : 0.0;
                 obj = sg.sum_f64(lane < M ? g : 0.0) + kc * hmax;
                 obj = obj + tsum;
                 obj = obj + xsum;
