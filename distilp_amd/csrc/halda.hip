@@ -3104,9 +3104,12 @@ template <class SG>
 __device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
                                           double &xsum, double &kappa) {
     const bool act = sg.sl < M;
-    tsum = sg.sum_f64(act ? mf.tcomm : 0.0);
-    xsum = sg.sum_f64(act ? xi_term(mf) : 0.0);
-    const double tail = sg.sum_f64(act ? tail_term(mf) : 0.0);
+    // one wave sum for the three per-device constants of obj_value (t_comm, xi and kappa's tail term,
+    // added per device in that order): tsum carries all of it, xsum is 0 and kappa its head terms;
+    // obj_value's constants are summed in this fixed order (the host recomputes the reference's own
+    // order for halda_solve)
+    tsum = sg.sum_f64(act ? (mf.tcomm + xi_term(mf)) + tail_term(mf) : 0.0);
+    xsum = 0.0;
     int hi = sg.lowest(act && (mf.flags & HALDA_DEV_HEAD));
     if (hi >= SG::S) hi = 0;
     // kappa_head's four quotients on lanes 0..3 of the problem (one division for the four), summed in
@@ -3123,7 +3126,7 @@ __device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields
     total += q1;
     total += q2;
     total += q3;
-    kappa = total + tail;
+    kappa = total;
 }
 
 __device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
