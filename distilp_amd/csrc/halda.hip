@@ -3178,6 +3178,8 @@ struct SweepArgs {
     int launch_id;
     int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
     int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
+    int xz;                        // 1: x / c of non-optimal instances written as zeros; 0: left as they are
+                                   // (the host zero-copy path zero-fills them on the host)
     int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
     unsigned char *gtab;           // kGlobal: per-wave slices
     int64_t gstride;
@@ -3301,7 +3303,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
         if (A.out.status) A.out.status[inst] = stj;
     }
-    if (A.out.x || A.out.c) {  // x / c of a settled instance are zero
+    if (A.xz && (A.out.x || A.out.c)) {  // x / c of a settled instance are zero
         uint64_t settled = sg.bits(kl && stj != kOpen);
         const int N = 7 * M + 1;
         while (settled) {
@@ -3515,7 +3517,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             best = obj;
             best_k = k;
         }
-        if (st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
+        if (A.xz && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
             const int N = 7 * M + 1;
             for (int cc = lane; cc < N; cc += S) {
                 if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
@@ -3766,6 +3768,7 @@ struct Ctx {
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
     bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
+    bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
     bool last_fleet_fused = false;
     void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
     size_t fflag_bytes = 0;
@@ -4031,6 +4034,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     A.mmax = mmax;
     A.uM = F.min_devices == F.max_devices ? F.max_devices : 0;
     A.k1dp = c->k1_force_dp ? 1 : 0;
+    A.xz = c->x_zero ? 1 : 0;
     A.r1max = int(r1max);
     A.tab = int(tab);
     A.tab_kc = int(tab_kc);
@@ -4512,7 +4516,12 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     r.status = reinterpret_cast<int32_t *>(base + o_st);
     r.x = out_h->x ? reinterpret_cast<double *>(base + o_x) : nullptr;
     r.c = out_h->c ? reinterpret_cast<double *>(base + o_c) : nullptr;
+    // zero-copy through the fused sweep: the kernels skip the zero x / c of non-optimal instances
+    // (stores across PCIe, most of a one-fleet k-sweep's time); the copy-out below zero-fills them
+    const bool host_zero = zc && c->fleets_fused && (r.x || r.c);
+    c->x_zero = !host_zero;
     const int rc = halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
+    c->x_zero = true;
     if (rc != HALDA_OK) return rc;
     if (zc) {
         HIP_TRY(hipEventRecord(c->ev_host, s));
@@ -4534,8 +4543,23 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     HIP_TRY(down(out_h->n, o_n, 4 * nd));
     HIP_TRY(down(out_h->obj_by_k, o_obk, 8 * nf * n_k));
     HIP_TRY(down(out_h->status, o_st, 4 * nf * n_k));
-    HIP_TRY(down(out_h->x, o_x, 8 * xs));
-    HIP_TRY(down(out_h->c, o_c, 8 * xs));
+    if (host_zero) {
+        // per (fleet, k): the kernel's x / c where the instance is optimal, zeros elsewhere
+        const size_t per = xs / (size_t(nf) * n_k);
+        const int32_t *st = reinterpret_cast<const int32_t *>(pin + o_st);
+        for (size_t i = 0; i < size_t(nf) * n_k; ++i) {
+            const bool opt = st[i] == HALDA_STATUS_OPTIMAL;
+            for (int a = 0; a < 2; ++a) {
+                double *dst = a == 0 ? out_h->x : out_h->c;
+                if (!dst) continue;
+                if (opt) std::memcpy(dst + i * per, pin + (a == 0 ? o_x : o_c) + 8 * i * per, 8 * per);
+                else std::memset(dst + i * per, 0, 8 * per);
+            }
+        }
+    } else {
+        HIP_TRY(down(out_h->x, o_x, 8 * xs));
+        HIP_TRY(down(out_h->c, o_c, 8 * xs));
+    }
     return HALDA_OK;
 }
 
