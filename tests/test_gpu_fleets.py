@@ -133,3 +133,28 @@ def test_fleet_sweep_per_k_objectives(llama_online_model):
         x = host.x[ref.col_off:ref.col_off + ref.n_cols]
         want = lowered[ref.fleet].objective_value(ref.c, x)
         assert abs(res.obj_by_k[ref.fleet, j] - want) <= 1e-12 * max(1.0, abs(want))
+
+
+def test_host_zero_copy_x_of_infeasible_k_are_zero(llama_online_model):
+    """The host zero-copy path (small synchronous calls): the fused sweep leaves the x / c of
+    non-optimal (fleet, k) instances unwritten in the pinned buffer and the copy-out zero-fills
+    them. Two different batches in a row (the second would see the first's x / c if the fill were
+    missing): non-optimal rows all zero, optimal rows equal to a large call's (device staging)."""
+    ctx = get_context(0)
+    for seeds, M in (([500, 501], 64), ([502, 503, 504], 12)):
+        fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)] for s in seeds]
+        table = fleet_table(fleets, llama_online_model)
+        small = solve_table(table, llama_online_model, KS80, 0.5, want_x=True)
+        N = 7 * M + 1
+        for f in range(len(seeds)):
+            for j in range(len(KS80)):
+                if small.status[f, j] != 0:
+                    assert not small.x[f, j].any() and not small.c[f, j].any(), (f, KS80[j])
+        assert (small.status == 0).any() and (small.status != 0).any()
+        # the same fleets inside a batch too large for the zero-copy path: same statuses and x / c
+        big_fleets = fleets + [[DeviceProfile.model_validate(d) for d in synth_fleet(600 + i, M)] for i in range(300)]
+        big = solve_table(fleet_table(big_fleets, llama_online_model), llama_online_model, KS80, 0.5, want_x=True)
+        n = len(seeds)
+        assert np.array_equal(big.status[:n], small.status)
+        assert np.array_equal(big.x[:n, :, :N], small.x[:, :, :N]) and np.array_equal(big.c[:n, :, :N], small.c[:, :, :N])
+    assert ctx is not None
