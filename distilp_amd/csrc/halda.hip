@@ -1816,20 +1816,25 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
             bad = bad || sg.bits(fin && lane < take && dt < dlast - 1e-12 * fmax(1.0, fabs(Gt))) != 0;
         }
         if (bad) return K1_FALLBACK;
-        // winner's new state: e = ew + take; G(e) and G(e + 1) from the evaluated window
+        // winner's new state: e = ew + take; G(e) from the evaluated window, and G(e + 1) / the last
+        // increment for the next round only when there is one (need > take; uniform)
         const double gcur = take == 1 ? gnw : sg.bcast(Gt, take - 2);
         const int ncur = take == 1 ? nNw : sg.bcast(nt, take - 2);
-        const double gnext = need > 1 ? sg.bcast(Gt, take - 1) : kInf;
-        const int nnext = need > 1 ? sg.bcast(nt, take - 1) : 0;
-        const double tlast = take == 1 ? bv : sg.bcast(dt, take - 2);
         if (lane == win) {
             e = ew + take;
             gE = gcur;
             nE = ncur;
-            gn = gnext;
-            nN = nnext;
-            inc = gnext < kInf ? gnext - gcur : kInf;
-            dprev = tlast;
+        }
+        if (need > take) {  // then need > 1: the window was evaluated
+            const double gnext = sg.bcast(Gt, take - 1);
+            const int nnext = sg.bcast(nt, take - 1);
+            const double tlast = take == 1 ? bv : sg.bcast(dt, take - 2);
+            if (lane == win) {
+                gn = gnext;
+                nN = nnext;
+                inc = gnext < kInf ? gnext - gcur : kInf;
+                dprev = tlast;
+            }
         }
         need -= take;
     }
