@@ -206,3 +206,49 @@ def test_register_launches_overlap_on_two_streams(llama_online_model):
         assert np.array_equal(d.out["best_k"].cpu().numpy(), w.best_k)
         assert np.array_equal(d.out["w"].cpu().numpy(), w.w) and np.array_equal(d.out["n"].cpu().numpy(), w.n)
         assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)
+
+
+@pytest.mark.parametrize("M", [64, 12])
+def test_uniform_fleets_viewed_from_an_offset_dev_off(llama_online_model, M):
+    """A device-resident table viewed from fleet 7 on (dev_off pointing into the middle, so dev_off[0]
+    != 0, the field arrays unchanged): with one fleet size the sweep issues the field loads from
+    dev_off[0] = 0 and reloads when the read of dev_off[0] says otherwise. Results equal the whole
+    table's for those fleets (w / n at the same absolute device indices)."""
+    import ctypes
+
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable, HaldaFleetResultC, HaldaFleetsC, _bind
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    table = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(700 + s, M)] for s in range(40)],
+                        llama_online_model)
+    dt = DeviceFleetTable(table, llama_online_model, ks, 0.5, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    dt.launch(ctx, stream)
+    torch.cuda.synchronize(dev)
+    full = {k: v.cpu().numpy() for k, v in dt.out.items()}
+    skip = 7
+    fs = HaldaFleetsC.from_buffer_copy(dt.fs)
+    fs.n_fleets = table.n_fleets - skip
+    fs.dev_off = dt.arrs["dev_off"].data_ptr() + 8 * skip
+    out = {"best_k": torch.zeros(fs.n_fleets, dtype=torch.int32, device=dev),
+           "obj_value": torch.zeros(fs.n_fleets, dtype=torch.float64, device=dev),
+           "w": torch.full((table.n_devices,), -1, dtype=torch.int32, device=dev),
+           "n": torch.full((table.n_devices,), -1, dtype=torch.int32, device=dev)}
+    res = HaldaFleetResultC(out["best_k"].data_ptr(), out["obj_value"].data_ptr(), out["w"].data_ptr(),
+                            out["n"].data_ptr(), None, None, None, None)
+    lib = _bind(ctx.lib)
+    with ctx._lock:
+        rc = lib.halda_solve_fleets(ctx.ctx, ctypes.byref(dt.model), ctypes.byref(fs), dt.ks.ctypes.data,
+                                    len(dt.ks), ctypes.byref(res), ctypes.c_void_p(stream))
+    assert rc == 0
+    torch.cuda.synchronize(dev)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    assert np.array_equal(got["best_k"], full["best_k"][skip:])
+    assert np.array_equal(got["obj_value"], full["obj_value"][skip:])
+    d0 = skip * M
+    assert np.array_equal(got["w"][d0:], full["w"][d0:]) and np.array_equal(got["n"][d0:], full["n"][d0:])
+    assert (got["w"][:d0] == -1).all()  # devices of the fleets outside the view are untouched
