@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # VALU instructions per wave of halda_sweep_kernel on the C3 workload (one wave = one M = 64 fleet):
 # SQ_INSTS_VALU / SQ_WAVES from rocprofv3 (profiles/r02_sq_counters.txt); a wave64 VALU instruction holds
 # its SIMD for >= 4 cycles (FP64 add / mul / FMA issue at full rate), 1,024 SIMDs at <= 2.4 GHz.
-SWEEP_VALU_PER_WAVE = 954
+SWEEP_VALU_PER_WAVE = 934
 VALU_CYCLES = 4
 N_SIMDS = 1024
 CLOCK_GHZ = 2.4

@@ -1790,10 +1790,11 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         const double m2 = sg.min_f64(rv);
         const int d2 = sg.lowest(act && lane != win && rv == m2);
         const int ew = sg.bcast(e, win), nNw = sg.bcast(nN, win);
-        const double gnw = sg.bcast(gn, win), dpw = sg.bcast(dprev, win);
+        const double gnw = sg.bcast(gn, win);
         // the winner takes its next increment bv; lane t evaluates G_win(ew + 2 + t)
         int take = 1;
-        bool bad = bv < dpw - 1e-12 * fmax(1.0, fabs(gnw));
+        // convexity against the winner's last taken increment (none in the first round: -inf)
+        bool bad = rounds > 1 && bv < sg.bcast(dprev, win) - 1e-12 * fmax(1.0, fabs(gnw));
         double Gt = kInf, dt = kInf;
         int nt = 0;
         if (need > 1) {
