@@ -48,11 +48,11 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-# The sweep kernel is bound by FP64 VALU issue, not HBM: its VALU roof beside the HBM one.
-# VALU instructions per wave of halda_sweep_kernel on the C3 workload (one wave = one M = 64 fleet):
-# SQ_INSTS_VALU / SQ_WAVES from rocprofv3 (profiles/r02_sq_counters.txt); a wave64 VALU instruction holds
-# its SIMD for >= 4 cycles (FP64 add / mul / FMA issue at full rate), 1,024 SIMDs at <= 2.4 GHz.
-SWEEP_VALU_PER_WAVE = 934
+# FP64-VALU-issue roof beside the HBM one: a wave64 VALU instruction holds its SIMD for >= 4
+# cycles (FP64 add / mul / FMA issue at full rate), 1,024 SIMDs at <= 2.4 GHz. The VALU count per wave is
+# NOT a constant here: it is read from the newest profiles/*_valu.json whose libhalda.so hash equals the
+# library this process loads (tools/valu_stamp.py writes it from a rocprofv3 SQ_INSTS_VALU / SQ_WAVES pass);
+# with no matching profile the VALU roof is reported as null.
 VALU_CYCLES = 4
 N_SIMDS = 1024
 CLOCK_GHZ = 2.4
@@ -266,25 +266,76 @@ def to_device(batch, torch, dev):
     return keep, out
 
 
-def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None):
+def lib_sha256() -> str:
+    """sha256 of the libhalda.so this process loads (keys the VALU-count profiles to a build)."""
+    import hashlib
+
+    from distilp_amd.solver._libhalda import LIB_PATH
+
+    return hashlib.sha256(Path(LIB_PATH).read_bytes()).hexdigest()
+
+
+def valu_profile(kernel: str, workload: str):
+    """{valu_per_wave, waves, ...} of `kernel` on `workload` ("c3" / "c2") from the newest
+    profiles/*_valu.json (tools/valu_stamp.py) recorded for THIS libhalda.so build, else None."""
+    sha = lib_sha256()
+    for c in sorted((REPO / "profiles").glob("r*_valu.json"), reverse=True):
+        try:
+            j = json.loads(c.read_text())
+            if j.get("libhalda_sha256") != sha:
+                continue
+            e = j["workloads"][workload][kernel]
+            return dict(e, source=f"profiles/{c.name}")
+        except Exception:  # noqa: BLE001
+            continue
+    return None
+
+
+def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None, workload="c3"):
     """Roofline of the dominant launch. phase_ms: per-launch device times (HIP events around each
     launch, one launch at a time). one_launch_ms: when every step is that one launch, its mean time
-    from HIP events around K back-to-back launches on its stream (no per-launch instrumentation)."""
+    from HIP events around K back-to-back launches on ONE stream (no per-launch instrumentation, no
+    overlap with another batch). Two roofs are reported as peers: HBM (algorithmic bytes / kernel time /
+    8 TB/s) and FP64-VALU issue (profiled VALU per wave x waves x 4 cycles / (1,024 SIMDs x 2.4 GHz x
+    kernel time)); `bound` keeps the contract's vocabulary (the kernel's memory roof), `nearest_roof`
+    names the larger fraction."""
     dom = max(phase_ms, key=phase_ms.get)
     alg = alg_bytes.get(dom)
     single = one_launch_ms is not None and single_launch_steps(phase_ms)
     ms = one_launch_ms if single else phase_ms[dom]
     achieved = alg / (ms * 1e-3) / 1e9 if alg else None
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic_fn(dom), "kernel": dom,
-            "kernel_ms": ms, "kernel_ms_from": ("HIP events around K back-to-back launches on one stream" if single
-                                                else "HIP events around each launch"),
-            "algorithmic_bytes_per_launch": alg, "launch_ms": phase_ms}
+    frac = achieved / HBM_PEAK_GBS if achieved else None
+    vp = valu_profile(dom, workload)
+    if vp:
+        need = vp["valu_per_wave"] * vp["waves"] * VALU_CYCLES / (N_SIMDS * CLOCK_GHZ * 1e9)
+        valu = {"frac": need / (ms * 1e-3), "valu_per_wave": vp["valu_per_wave"], "waves": vp["waves"],
+                "cycles_per_valu": VALU_CYCLES, "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": vp["source"],
+                "wait_any_frac": vp.get("wait_any_frac"),
+                "what": "FP64-VALU-issue roof of the same launch: VALU cycles its waves need / SIMD cycles in the "
+                        "kernel time (rocprofv3 SQ_INSTS_VALU / SQ_WAVES of this build, peak clock)"}
+    else:
+        valu = {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
+    roofs = {"hbm": frac, "valu_issue": valu["frac"]}
+    nearest = max((k for k, v in roofs.items() if v is not None), key=lambda k: roofs[k], default=None)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": frac,
+            "traffic": traffic_fn(dom), "kernel": dom, "kernel_ms": ms,
+            "kernel_ms_from": ("HIP events around K back-to-back launches on one stream" if single
+                               else "HIP events around each launch"),
+            "algorithmic_bytes_per_launch": alg, "roofs": roofs, "nearest_roof": nearest, "valu_issue": valu,
+            "launch_ms": phase_ms}
 
 
 def single_launch_steps(phase_ms):
     dom = max(phase_ms, key=phase_ms.get)
     return all(v < 1e-3 for k, v in phase_ms.items() if k != dom)
+
+
+def sweep_bytes(table) -> int:
+    """Algorithmic bytes of one fused k-sweep launch over `table`: per fleet its device
+    fields (130 B per device) and dev_off (8 B) in; best k (4 B), obj_value (8 B) and w / n (8 B per
+    device) out."""
+    sizes = table.sizes()
+    return int(sum(DEV_FIELDS * int(m) + 8 + 4 + 8 + 8 * int(m) for m in sizes))
 
 
 def timed_events(step, steps, torch, dev, stream):
@@ -353,6 +404,61 @@ def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
             "target_instances_per_s": 10_000}
 
 
+def c2_leg(args, torch, dev, ctx, model, stream, srefs):
+    """Config C2 (BASELINE.json configs[1]) as its own leg: 4096 synthetic M = 16 fleets x every k of
+    L = 80 (k = 1, 2, 4, 5 feasible: the k > 1 MILPs of halda_p_solver.py:391-412 are solved here), one
+    halda_solve_fleets k-sweep per step from resident tables; its own roofline from the one-stream launch
+    time of its dominant kernel."""
+    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table
+
+    M2 = 16
+    table = fleet_table(build_fleets(range(C3_FLEETS), M2), model)
+    n = max(2, min(32, math.ceil(2 * MALL_BYTES / max(DeviceFleetTable(table, model, KS_L80, 0.5, dev).nbytes(), 1))))
+    tabs = [DeviceFleetTable(table, model, KS_L80, 0.5, dev, want_per_k=True) for _ in range(n)]
+    turn = [0]
+
+    def step2():
+        tabs[turn[0] % n].launch(ctx, srefs[turn[0] % 2])
+        turn[0] += 1
+
+    def step1():
+        tabs[turn[0] % n].launch(ctx, stream.cuda_stream)
+        turn[0] += 1
+
+    ctx.set_timing(False)
+    for _ in range(max(2, args.warmup)):
+        step1()
+    torch.cuda.synchronize(dev)
+    st = tabs[(turn[0] - 1) % n].out["status"].cpu().numpy()
+    n_opt = int((st == 0).sum())
+    bk = tabs[(turn[0] - 1) % n].out["best_k"].cpu().numpy()
+    if not (bk > 0).all():
+        raise RuntimeError("C2: a fleet without a feasible k")
+    steps = max(10, args.steps // 4)
+    el2 = timed(step2, steps, torch, dev, None, 1)
+    ev1 = timed_events(step1, steps, torch, dev, stream)
+    ctx.set_timing(True)
+    per = []
+    for _ in range(5):
+        step1()
+        torch.cuda.synchronize(dev)
+        per.append(ctx.last_fleet_ms())
+    ctx.set_timing(False)
+    ph = {k: statistics.mean(p.get(k, 0.0) for p in per) for k in per[0]}
+    alg = sweep_bytes(table)
+    inst = C3_FLEETS * len(KS_L80)
+    return {
+        "workload": f"C2: {C3_FLEETS} synthetic M={M2} fleets x {len(KS_L80)} k-candidates (L=80, llama_3_70b/online, "
+                    "kv 4bit) per step, one halda_solve_fleets k-sweep from resident tables",
+        "instances_per_step": inst, "feasible_per_step": n_opt,
+        "ms_per_step_one_stream": ev1, "instances_per_s_one_stream": inst / (ev1 * 1e-3),
+        "ms_per_step_two_streams": el2 / steps * 1e3, "instances_per_s_two_streams": inst * steps / el2,
+        "steps": steps, "resident_copies": n,
+        "roofline": roofline(ph, {k: alg for k in ph}, lambda k: None, ev1 if single_launch_steps(ph) else None,
+                             workload="c2"),
+    }
+
+
 def launch_ranks(args) -> int:
     """--gpus N from a plain `python bench.py`: start N ranks (one process per GPU) with
     torch.distributed.run before this process touches the GPU, relay their output and exit code."""
@@ -384,6 +490,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tto", action="store_true")
+    ap.add_argument("--no-c2", action="store_true", help="skip the config-2 leg (4096 M = 16 fleets)")
     ap.add_argument("--ks", type=str, default="", help="diagnostic: comma-separated k-candidates instead of C3's")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-core", type=int, default=0)
@@ -531,6 +638,9 @@ def main():
     total = inst_rank * world * args.steps if not strong_head else C3_FLEETS * len(ks) * args.steps
     value = total / el_sweep
     n_fleets_total = (len(fleets) * world if not strong_head else C3_FLEETS) * args.steps
+    c2 = None
+    if world == 1 and not args.no_c2:
+        c2 = c2_leg(args, torch, dev, ctx, model, stream, srefs)
     if rank == 0:
         tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
@@ -577,23 +687,21 @@ def main():
                 "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,
                 "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
             },
+            "c2": c2,
             "c5_stream": c5,
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,
         }
         rf = line["roofline"]
         if rf["algorithmic_bytes_per_launch"] and single_launch_steps(fl_mean):
-            # the same bytes over the pipelined step time (two streams: batches overlap on the device)
+            # two independent batches in flight on two streams: the step is shorter than one launch, so
+            # this is throughput over overlapped launches, never a kernel fraction
             a = rf["algorithmic_bytes_per_launch"] / (line["ms_per_step"] * 1e-3) / 1e9
-            rf["pipelined"] = {"achieved": a, "frac": a / HBM_PEAK_GBS, "ms_per_step": line["ms_per_step"]}
-            if rf["kernel"] == "halda_sweep_kernel" and args.M == 64 and ks == KS_L80:
-                need = len(fleets) * SWEEP_VALU_PER_WAVE * VALU_CYCLES / (N_SIMDS * CLOCK_GHZ * 1e9)
-                rf["valu_issue"] = {
-                    "what": "FP64-VALU-issue roof of the same launch: VALU cycles its waves need / SIMD cycles "
-                            "in the launch time (profiled VALU count, peak clock)",
-                    "valu_per_wave": SWEEP_VALU_PER_WAVE, "waves": len(fleets), "cycles_per_valu": VALU_CYCLES,
-                    "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": "profiles/r02_sq_counters.txt",
-                    "frac": need / (rf["kernel_ms"] * 1e-3), "frac_pipelined": need / (line["ms_per_step"] * 1e-3)}
+            line["throughput_overlap"] = {
+                "what": "the headline steps: consecutive batches alternate over two streams, so one batch's field "
+                        "loads overlap the previous batch's compute; algorithmic bytes of one launch over that "
+                        "step time (not a kernel roofline: the kernel itself takes roofline.kernel_ms)",
+                "ms_per_step": line["ms_per_step"], "kernel_ms": rf["kernel_ms"], "alg_GBps_over_step": a}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

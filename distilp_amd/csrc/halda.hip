@@ -3195,17 +3195,26 @@ struct SweepArgs {
 
 // x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
 // by the lane of each device when the caller asked for them.
+// Element offset of instance inst's x / c: the dense layout, or the caller's compact x_off (-1: not
+// written).
+__device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
+    return A.out.x_off ? A.out.x_off[inst] : inst * A.xstride;
+}
+
 __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
                               const FieldRec &r) {
+    if (!A.out.x && !A.out.c) return;
+    const int64_t at = xc_at(A, inst);
+    if (at < 0) return;
     const Dev d = r.dev();
     if (A.out.x) {
-        double *x = A.out.x + inst * A.xstride;
+        double *x = A.out.x + at;
         x[i] = double(wl); x[M + i] = double(n);
         x[2 * M + i] = double(s[0]); x[3 * M + i] = double(s[1]); x[4 * M + i] = double(s[2]);
         x[5 * M + i] = double(s[3]); x[6 * M + i] = z;
     }
     if (A.out.c) {
-        double *c = A.out.c + inst * A.xstride;
+        double *c = A.out.c + at;
         c[i] = d.cw; c[M + i] = d.cn; c[2 * M + i] = d.cs0; c[3 * M + i] = d.cs1; c[4 * M + i] = d.cs2;
         c[5 * M + i] = d.cs3; c[6 * M + i] = 0.0;
     }
@@ -3216,7 +3225,9 @@ __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, in
 #endif
 
 __device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
-    if (lane == 0) {
+    // the scratch-free register launch (fflag == nullptr) never flags: sweep_fleets runs it alone only
+    // when nothing in the batch can need the table launch (no k > 1 with W >= M, R + 1 <= kDpLanes)
+    if (lane == 0 && A.fflag) {
         A.fflag[f] = 1;
         __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -3315,11 +3326,12 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         while (settled) {
             const int j = __builtin_ctzll(settled);
             settled &= settled - 1;
-            const int64_t inst = int64_t(f) * A.n_k + j;
-            for (int cc = lane; cc < N; cc += S) {
-                if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
-                if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
-            }
+            const int64_t at = xc_at(A, int64_t(f) * A.n_k + j);
+            if (at >= 0)
+                for (int cc = lane; cc < N; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
         }
     }
     uint64_t todo = sg.bits(kl && stj == kOpen);
@@ -3411,9 +3423,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                         A.out.n[d0 + lane] = n;
                     }
                 }
-                if (lane == 0) {
-                    if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
-                    if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
+                if (lane == 0 && (A.out.x || A.out.c)) {
+                    const int64_t at = xc_at(A, inst);
+                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
                 }
                 HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
             } else if constexpr (!kTables) {
@@ -3502,9 +3515,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                                 A.out.n[d0 + i] = n;
                             }
                         }
-                    if (lane == 0) {
-                        if (A.out.x) A.out.x[inst * A.xstride + 7 * M] = hmax;
-                        if (A.out.c) A.out.c[inst * A.xstride + 7 * M] = kc;
+                    if (lane == 0 && (A.out.x || A.out.c)) {
+                        const int64_t at = xc_at(A, inst);
+                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
                     }
                     HALDA_TSTAMP(8);
                 }
@@ -3514,9 +3528,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         if (st == HALDA_STATUS_OPTIMAL && M == 0) {
             obj = 0.0;  // c.x = 0; no devices: the offsets are empty sums and kappa is undefined
             improved = obj < best;
-            if (lane == 0) {
-                if (A.out.x) A.out.x[inst * A.xstride] = 0.0;
-                if (A.out.c) A.out.c[inst * A.xstride] = kc;
+            if (lane == 0 && (A.out.x || A.out.c)) {
+                const int64_t at = xc_at(A, inst);
+                if (at >= 0 && A.out.x) A.out.x[at] = 0.0;
+                if (at >= 0 && A.out.c) A.out.c[at] = kc;
             }
         }
         if (improved) {
@@ -3525,10 +3540,12 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         }
         if (A.xz && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
             const int N = 7 * M + 1;
-            for (int cc = lane; cc < N; cc += S) {
-                if (A.out.x) A.out.x[inst * A.xstride + cc] = 0.0;
-                if (A.out.c) A.out.c[inst * A.xstride + cc] = 0.0;
-            }
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = lane; cc < N; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
         }
         if (lane == 0) {
             if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
@@ -3671,6 +3688,255 @@ __global__ __launch_bounds__(64, HALDA_SEG_WAVES_PER_SIMD) void halda_sweep_seg_
     }
 }
 
+// halda_sweep_kslot_kernel: the k-sweep of fleets of at most kSegLanes devices (C2) with the k's
+// spread over waves. A workgroup holds four fleets (one per 16-lane segment, as the segment kernel)
+// and one wave per open k-slot (the k's some fleet of the batch can take: L / k >= min_devices,
+// L / k < 1e6, ascending); wave q solves k-slot q of its four fleets -- the k = 1 register greedy,
+// the forced W = M split, or the k > 1 tables + threshold scan in its own LDS slice -- and leaves its
+// objective, status and (w, n) in the workgroup's pick area. After one barrier, wave 0 picks each
+// fleet's best k by the reference's rule (ascending k, strict "<" on obj_value,
+// halda_p_solver.py:407) and writes best_k / obj_value / w / n; the k's no slot takes (settled for
+// every fleet: M > W or W >= 1e6) are written there too. Same per-(fleet, k) arithmetic as
+// sweep_fleet on Seg<16> (the same records, reductions and tie rules: the same bits), but the
+// segment kernel's one wave per four fleets becomes one wave per (four fleets, k): four to sixteen
+// times the waves to hide the reductions' and LDS round trips' latency. What the slot waves cannot
+// take (greedy fallbacks, tables beyond the slice, non-convex leaves) flags the fleet for the gated
+// table launch, which redoes it whole.
+constexpr int kMaxSlots = 16;
+constexpr int kSlotFlagged = 1000;  // SlotPick.st: the fleet goes to the table launch
+
+struct SlotPick {  // one (segment, k-slot) result in the workgroup's pick area
+    double obj;    // obj_value when OPTIMAL, else +inf
+    int st;        // HALDA_STATUS_* or kSlotFlagged
+    int pad;
+    int w[kSegLanes], n[kSegLanes];
+};
+
+struct SlotArgs {
+    int n_slot;
+    int pick_off;              // LDS byte offset of the pick area (SlotPick [4][n_slot])
+    int j[kMaxSlots];          // k index of slot q (ascending)
+    int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * (R + 1) + max_devices, 0: no tables
+    int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
+    int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
+};
+
+// One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
+// its w / n candidate).
+__device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tabcap, const WaveCtx &w,
+                            const Seg<kSegLanes> &sg, SlotPick *pk) {
+    using SG = Seg<kSegLanes>;
+    constexpr int S = SG::S;
+    const int lane = sg.sl;
+    const halda_model &Mo = A.Mo;
+    const halda_fleets &F = A.F;
+    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
+    const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+    int bad = 0;
+    FieldRec me = field_rec(Mo, mf, bad);
+    bad = lane < M ? bad : 0;
+    double tsum, xsum, kappa;
+    fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
+    const bool anybad = sg.any(bad != 0);
+    const int k = A.ks[j], W = A.Ws[j];
+    const int64_t inst = int64_t(f) * A.n_k + j;
+    const double kc = double(k - 1);
+    int st;
+    double obj = kInf;
+    int wl = 0, nl = 0;  // this lane's (w, n) in the solution
+    if (!(W < 1000000)) st = HALDA_STATUS_UNSUPPORTED;
+    else if (M > W) st = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
+    else if (anybad) st = HALDA_STATUS_UNSUPPORTED;
+    else {
+        me.W = W;
+        if (k == 1 || W == M) {
+            // the register greedy; W = M (R = 0): every w_i = 1 is forced
+            int e = 0, rounds = 0, nE = 0;
+            double gE = 0.0;
+            const int rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
+            if (rc == K1_INFEASIBLE) {
+                st = HALDA_STATUS_INFEASIBLE;
+            } else if (rc == K1_OK) {
+                double g = 0.0, H = 0.0, z = 0.0;
+                int n = 0, sl[4] = {0, 0, 0, 0};
+                wl = 1 + e;
+                const bool need_h = kc != 0.0 || A.out.x;
+                if (lane < M) {
+                    g = gE;
+                    n = nE;
+                    rec_slacks(me, wl, n, sl);
+                    if (need_h) {
+                        double P, Q;
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        z = Q > P ? 0.5 * (Q - P) : 0.0;
+                        H = Q >= P ? 0.5 * (P + Q) : P;
+                    }
+                }
+                const double hmax = need_h ? fmax(0.0, sg.max_f64(lane < M ? H : 0.0)) : 0.0;
+                obj = sg.sum_f64(lane < M ? g : 0.0) + kc * hmax;
+                obj = obj + tsum;
+                obj = obj + xsum;
+                obj = obj + kappa;
+                st = HALDA_STATUS_OPTIMAL;
+                nl = n;
+                if (lane < M) put_xc(A, inst, M, lane, wl, n, sl, z, me);
+                if (lane == 0 && (A.out.x || A.out.c)) {
+                    const int64_t at = xc_at(A, inst);
+                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                }
+            } else {
+                st = kSlotFlagged;  // a greedy fallback: the 64-lane table launch
+            }
+        } else if (M < 2) {
+            st = kSlotFlagged;
+        } else {
+            Inst I = {};
+            I.inst = int(inst);
+            I.M = M;
+            I.W = W;
+            I.Wd = double(W);
+            I.kc = kc;
+            I.iC = 7 * M;
+            I.R1 = W - M + 1;
+            I.RS = odd_stride(I.R1);
+            if (M > A.mmax || I.R1 > r1cap || int64_t(M) * I.RS > tabcap) {
+                st = kSlotFlagged;  // beyond the slot's slice
+            } else {
+                const FieldSrc src{&A.Mo, &A.F, &me, d0, W, sg.base};
+                int64_t nodes = 0;
+                table_pass<S>(src, w, I, lane);
+                wave_sync();
+                const int feas = dp_pass_lanes(w, I, sg, nodes);
+                if (feas < 0) {
+                    st = kSlotFlagged;  // a leaf the incremental scan does not take
+                } else if (!feas) {
+                    st = HALDA_STATUS_INFEASIBLE;
+                } else {
+                    double g = 0.0, P = 0.0, Q = 0.0, hmax = 0.0;
+                    int n = 0, sl[4] = {0, 0, 0, 0};
+                    if (lane < M) {
+                        wl = 1 + w.st0[lane];
+                        split_full(me, wl, g, n, sl);
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        hmax = Q >= P ? 0.5 * (P + Q) : P;
+                        put_xc(A, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
+                    }
+                    hmax = sg.max_f64(fmax(0.0, hmax));
+                    obj = sg.sum_f64(0.0 + g) + kc * hmax;  // the segment kernel's sum (0.0 + g per lane)
+                    obj = obj + tsum;
+                    obj = obj + xsum;
+                    obj = obj + kappa;
+                    st = HALDA_STATUS_OPTIMAL;
+                    nl = n;
+                    if (lane == 0 && (A.out.x || A.out.c)) {
+                        const int64_t at = xc_at(A, inst);
+                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                    }
+                }
+            }
+        }
+    }
+    if (st == kSlotFlagged) {
+        flag_fleet(A, f, lane);
+    } else {
+        if (lane == 0) {
+            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.out.status) A.out.status[inst] = st;
+        }
+        if (A.xz && st != HALDA_STATUS_OPTIMAL && (A.out.x || A.out.c)) {  // x / c of a non-optimal instance
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = lane; cc < 7 * M + 1; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+    }
+    if (lane == 0) {
+        pk->obj = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+        pk->st = st;
+    }
+    if (lane < M) {
+        pk->w[lane] = wl;
+        pk->n[lane] = nl;
+    }
+}
+
+// The pick of one fleet (segment lanes): best k over the slots in ascending k with strict "<", the
+// settled k's of no slot, best_k / obj_value / w / n and the fleet's flag byte.
+__device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const SlotPick *pk, const Seg<kSegLanes> &sg) {
+    constexpr int S = kSegLanes;
+    const int lane = sg.sl;
+    const int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + A.F.dev_off[0] : A.F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(A.F.dev_off[f + 1] - d0);
+    bool flagged = false;
+    double best = kInf;
+    int bq = -1;
+    for (int q = 0; q < SA.n_slot; ++q) {
+        const int st = pk[q].st;
+        flagged = flagged || st == kSlotFlagged;
+        if (st == HALDA_STATUS_OPTIMAL && pk[q].obj < best) {
+            best = pk[q].obj;
+            bq = q;
+        }
+    }
+    if (flagged) return;  // the table launch redoes this fleet (fflag / hb_flag set by the slot wave)
+    // k's of no slot: settled for every fleet of the batch (W >= 1e6 unsupported, else M > W)
+    for (int jj = lane; jj < A.n_k; jj += S) {
+        bool slot = false;
+        for (int q = 0; q < SA.n_slot; ++q) slot = slot || SA.j[q] == jj;
+        if (slot) continue;
+        const int64_t inst = int64_t(f) * A.n_k + jj;
+        const int st = !(A.Ws[jj] < 1000000) ? HALDA_STATUS_UNSUPPORTED : HALDA_STATUS_INFEASIBLE;
+        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
+        if (A.out.status) A.out.status[inst] = st;
+        if (A.xz && (A.out.x || A.out.c)) {
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = 0; cc < 7 * M + 1; ++cc) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+    }
+    if (lane == 0) {
+        A.out.best_k[f] = bq >= 0 ? A.ks[SA.j[bq]] : 0;
+        A.out.obj_value[f] = best;
+        A.fflag[f] = 0;
+    }
+    if (lane < M) {
+        A.out.w[d0 + lane] = bq >= 0 ? pk[bq].w[lane] : 0;
+        A.out.n[d0 + lane] = bq >= 0 ? pk[bq].n[lane] : 0;
+    }
+}
+
+__global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int kPer = 64 / kSegLanes;
+    const int lane = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // this wave's k-slot
+    const Seg<kSegLanes> sg(lane);
+    const int seg = lane / kSegLanes;
+    const int nf = A.F.n_fleets;
+    const int64_t f = int64_t(blockIdx.x) * kPer + seg;
+    SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
+    {
+        const int tab = SA.tab[q];
+        const int64_t tb = align16(int64_t(tab) * 8);
+        unsigned char *base = smem + SA.off[q] + int64_t(seg) * seg_slice_bytes(A.mmax, tab);
+        WaveCtx w = {};
+        w.G = reinterpret_cast<double *>(base);
+        w.H = reinterpret_cast<double *>(base + tb);
+        w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q);
+    }
+    __syncthreads();
+    if (q == 0 && f < nf) kslot_pick(A, SA, int(f), pick + seg * SA.n_slot, sg);
+}
+
 // halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
 // sum xi + kappa (halda_p_solver.py:356-357), best k by ascending k with strict
 // "<" (halda_p_solver.py:407), w / n of the winner (int(round(x)), :350-351).
@@ -3703,12 +3969,13 @@ __global__ __launch_bounds__(64) void halda_pick_kernel(halda_batch B, halda_res
             if (out.obj_by_k) out.obj_by_k[inst] = obj;
             if (out.status) out.status[inst] = st;
         }
-        if (out.x || out.c) {
+        const int64_t at = out.x_off ? out.x_off[inst] : inst * xstride;
+        if ((out.x || out.c) && at >= 0) {
             const int64_t co = B.col_off[inst];
             const int N = B.n_cols[inst];
             for (int cc = lane; cc < N; cc += 64) {
-                if (out.x) out.x[inst * xstride + cc] = st == HALDA_STATUS_OPTIMAL ? R.x[co + cc] : 0.0;
-                if (out.c) out.c[inst * xstride + cc] = st == HALDA_STATUS_OPTIMAL ? B.c[co + cc] : 0.0;
+                if (out.x) out.x[at + cc] = st == HALDA_STATUS_OPTIMAL ? R.x[co + cc] : 0.0;
+                if (out.c) out.c[at + cc] = st == HALDA_STATUS_OPTIMAL ? B.c[co + cc] : 0.0;
             }
         }
     }
@@ -3770,6 +4037,8 @@ struct Ctx {
     bool fleet_two = false;                      // fused sweep: a second launch was enqueued
     bool fleet_reg_alone = false;                // fused sweep: the register launch alone
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
+    bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
+    bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
@@ -3795,7 +4064,7 @@ struct Ctx {
     hipError_t occupancy(const void *fn, int64_t lds, int *per_cu) {
         for (int i = 0; i < n_occ; ++i)
             if (occ[i].fn == fn && occ[i].lds == lds) {
-                *per_cu = occ[i].per_cu;
+                if (per_cu) *per_cu = occ[i].per_cu;
                 return hipSuccess;
             }
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -3806,7 +4075,7 @@ struct Ctx {
         p = std::max(1, p);
         occ[n_occ % 8] = Occ{fn, lds, p};
         n_occ = std::min(n_occ + 1, 8);
-        *per_cu = p;
+        if (per_cu) *per_cu = p;
         return hipSuccess;
     }
 };
@@ -4001,12 +4270,36 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     // fleets of <= 16 devices needing k > 1 tables: the lane-segment launch (four fleets per wave),
     // then the table launch for what it flagged
     const int64_t seg_lds = seg_slice_bytes(mmax, int(tab_kc)) * (64 / kSegLanes);
-    const bool seg = c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
+    // k-slot launch (preferred): the same fleets, one wave per (four fleets, open k)
+    SlotArgs SA = {};
+    int64_t kslot_lds = 0;
+    for (int j = 0; j < n_k && SA.n_slot < kMaxSlots; ++j) {
+        const int W = model.L / kh[j];
+        if (!(W < 1000000) || W < F.min_devices) continue;  // settled for every fleet of the batch
+        const int q = SA.n_slot++;
+        SA.j[q] = j;
+        SA.r1[q] = W - F.min_devices + 1;
+        SA.tab[q] = kh[j] > 1 && W > F.min_devices ? mmax * SA.r1[q] + mmax : 0;
+        SA.off[q] = int(kslot_lds);
+        kslot_lds += (64 / kSegLanes) * seg_slice_bytes(mmax, SA.tab[q]);
+    }
+    bool kslot_all = true;  // every k that is open for some fleet has a slot
+    for (int j = 0, q = 0; j < n_k; ++j) {
+        const int W = model.L / kh[j];
+        if (!(W < 1000000) || W < F.min_devices) continue;
+        kslot_all = kslot_all && q < SA.n_slot && SA.j[q] == j;
+        ++q;
+    }
+    SA.pick_off = int(kslot_lds);
+    kslot_lds += int64_t(64 / kSegLanes) * SA.n_slot * int64_t(sizeof(SlotPick));
+    const bool kslot = c->seg_sweep && c->kslot_sweep && fits && mmax <= kSegLanes && tab_kc > 0 && kslot_all &&
+                       SA.n_slot >= 1 && nf > kSweepSmallBatch && kslot_lds <= kLdsBudget;
+    const bool seg = !kslot && c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
                      nf > kSweepSmallBatch && seg_lds <= kLdsBudget;
     // small batches (a single halda_solve) take one launch: the register kernel when it needs no table
     // launch behind it, else the table kernel alone
     const bool small_tables = nf <= kSweepSmallBatch && r1_k1 > kDpLanes;
-    const bool reg_mode = !seg && !(fits && (tables_first || small_tables));
+    const bool reg_mode = !seg && !kslot && !(fits && (tables_first || small_tables));
     // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
     // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
     const bool gate = tables_first || r1_k1 > kDpLanes;
@@ -4047,7 +4340,21 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     c->fleet_timed = false;
     c->have_lowered = false;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    if (seg) {
+    if (kslot) {
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_kslot_kernel), kslot_lds, nullptr));
+        const int64_t groups = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
+        A.want = 0;
+        hipLaunchKernelGGL(halda_sweep_kslot_kernel, dim3(unsigned(groups)), dim3(64 * SA.n_slot), size_t(kslot_lds), s,
+                           A, SA);
+        HIP_TRY(hipGetLastError());
+        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
+        A.want = 1;
+        int per_cu = 0;
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
+        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(unsigned(std::min<int64_t>(c->cus, nf))), dim3(64),
+                           size_t(slice), s, A);
+        HIP_TRY(hipGetLastError());
+    } else if (seg) {
         int per_cu = 0;
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_seg_kernel), seg_lds, &per_cu));
         const int64_t nw = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
@@ -4109,9 +4416,10 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = seg || (reg_mode && gate);
+    c->fleet_two = seg || kslot || (reg_mode && gate);
     c->fleet_reg_alone = reg_mode && !gate;
     c->fleet_seg = seg;
+    c->fleet_kslot = kslot;
     c->last_fleet_fused = true;
     return HALDA_OK;
 }
@@ -4255,10 +4563,12 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
 int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    if (path < 0 || path > 3)
-        return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave) or 3 (fused, k = 1 by DP)");
+    if (path < 0 || path > 4)
+        return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave), 3 (fused, k = 1 "
+                                 "by DP) or 4 (fused, segment kernel instead of the k-slot kernel)");
     c->fleets_fused = path != 0;
-    c->seg_sweep = path == 1;
+    c->seg_sweep = path == 1 || path == 4;
+    c->kslot_sweep = path == 1;
     c->k1_force_dp = path == 3;
     return HALDA_OK;
 }
@@ -4268,13 +4578,13 @@ int halda_last_fleet_ms(void *ctx, double *ms8) {
     if (!c || !ms8) return fail(HALDA_E_ARG, "NULL ctx/ms");
     if (!c->fleet_timed) return fail(HALDA_E_ARG, "no timed halda_solve_fleets call on this context");
     HIP_TRY(hipEventSynchronize(c->evf1));
-    for (int i = 0; i < 8; ++i) ms8[i] = 0.0;
+    for (int i = 0; i < 9; ++i) ms8[i] = 0.0;
     if (c->last_fleet_fused) {
         float a = 0.f, b = 0.f;
         if (c->fleet_two) {
             HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evfm));
             HIP_TRY(hipEventElapsedTime(&b, c->evfm, c->evf1));
-            ms8[c->fleet_seg ? 7 : 0] = a;
+            ms8[c->fleet_kslot ? 8 : c->fleet_seg ? 7 : 0] = a;
             ms8[1] = b;
         } else {
             HIP_TRY(hipEventElapsedTime(&a, c->evf0, c->evf1));
@@ -4453,9 +4763,24 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_doff = take(8 * (nf + 1)), o_cls = take(nd), o_fl = take(nd), o_f64 = take(8 * nd * 10),
-                 o_i64 = take(8 * nd * 6), o_bk = take(4 * nf), o_obj = take(8 * nf), o_w = take(4 * nd),
+                 o_i64 = take(8 * nd * 6);
+    const bool xsel = out_h->x_off && (out_h->x || out_h->c);
+    const size_t o_xoff = xsel ? take(8 * size_t(nf) * n_k) : 0;
+    const size_t o_bk = take(4 * nf), o_obj = take(8 * nf), o_w = take(4 * nd),
                  o_n = take(4 * nd), o_obk = take(8 * nf * n_k), o_st = take(4 * nf * n_k);
-    const size_t xs = size_t(nf) * n_k * (7 * size_t(std::max(fh->max_devices, 1)) + 1);
+    // x / c extent: the dense layout, or the caller's compact one (x_off, host memory)
+    size_t xs = size_t(nf) * n_k * (7 * size_t(std::max(fh->max_devices, 1)) + 1);
+    if (xsel) {
+        int64_t ext = 0;
+        for (int64_t f = 0; f < nf; ++f) {
+            const int64_t N = 7 * (fh->dev_off[f + 1] - fh->dev_off[f]) + 1;
+            for (int j = 0; j < n_k; ++j) {
+                const int64_t a = out_h->x_off[f * n_k + j];
+                if (a >= 0) ext = std::max(ext, a + N);
+            }
+        }
+        xs = size_t(ext);
+    }
     const size_t o_x = out_h->x ? take(8 * xs) : 0, o_c = out_h->c ? take(8 * xs) : 0;
     if (off > c->scratch_bytes) {
         if (c->scratch) HIP_TRY(hipFree(c->scratch));
@@ -4496,13 +4821,14 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     // small calls (a single halda_solve: ~8 KB in, ~70 KB out) skip both copies: the kernels read the
     // table from and write the results to the pinned buffer itself, across PCIe, and the host polls
     // the completion event instead of sleeping in a stream synchronisation
+    if (xsel) HIP_TRY(up(o_xoff, out_h->x_off, 8 * size_t(nf) * n_k));
     const bool zc = off <= kZeroCopyBytes;
     if (zc) {
         void *dp = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
         base = static_cast<char *>(dp);
     } else {
-        HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));  // the table (and x_off)
     }
     auto F64 = [&](int a) { return reinterpret_cast<const double *>(base + o_f64 + 8 * nd * a); };
     auto I64 = [&](int a) { return reinterpret_cast<const int64_t *>(base + o_i64 + 8 * nd * a); };
@@ -4522,9 +4848,10 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     r.status = reinterpret_cast<int32_t *>(base + o_st);
     r.x = out_h->x ? reinterpret_cast<double *>(base + o_x) : nullptr;
     r.c = out_h->c ? reinterpret_cast<double *>(base + o_c) : nullptr;
+    r.x_off = xsel ? reinterpret_cast<const int64_t *>(base + o_xoff) : nullptr;
     // zero-copy through the fused sweep: the kernels skip the zero x / c of non-optimal instances
     // (stores across PCIe, most of a one-fleet k-sweep's time); the copy-out below zero-fills them
-    const bool host_zero = zc && c->fleets_fused && (r.x || r.c);
+    const bool host_zero = zc && c->fleets_fused && (r.x || r.c) && !xsel;
     c->x_zero = !host_zero;
     const int rc = halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
     c->x_zero = true;
@@ -4610,7 +4937,7 @@ int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_f
     const int nd = int(m->ctxs.size()), nf = fh->n_fleets;
     if (nf <= 0) return HALDA_OK;
     const int64_t xs = 7 * int64_t(std::max(fh->max_devices, 1)) + 1;
-    std::vector<std::vector<int64_t>> offs(nd);
+    std::vector<std::vector<int64_t>> offs(nd), xoffs(nd);
     std::vector<int> rcs(nd, HALDA_OK);
     std::vector<std::string> errs(nd);
     std::vector<std::thread> th;
@@ -4640,8 +4967,21 @@ int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_f
             o.n = out_h->n + d0;
             o.obj_by_k = out_h->obj_by_k ? out_h->obj_by_k + int64_t(lo) * n_k : nullptr;
             o.status = out_h->status ? out_h->status + int64_t(lo) * n_k : nullptr;
-            o.x = out_h->x ? out_h->x + int64_t(lo) * n_k * xs : nullptr;
-            o.c = out_h->c ? out_h->c + int64_t(lo) * n_k * xs : nullptr;
+            if (out_h->x_off) {  // compact layout: the block's offsets relative to its first slot
+                int64_t b0 = INT64_MAX;
+                for (int64_t i = int64_t(lo) * n_k; i < int64_t(hi) * n_k; ++i)
+                    if (out_h->x_off[i] >= 0) b0 = std::min(b0, out_h->x_off[i]);
+                if (b0 == INT64_MAX) b0 = 0;
+                xoffs[r].resize(size_t(hi - lo) * size_t(n_k));
+                for (int64_t i = int64_t(lo) * n_k; i < int64_t(hi) * n_k; ++i)
+                    xoffs[r][size_t(i - int64_t(lo) * n_k)] = out_h->x_off[i] >= 0 ? out_h->x_off[i] - b0 : -1;
+                o.x_off = xoffs[r].data();
+                o.x = out_h->x ? out_h->x + b0 : nullptr;
+                o.c = out_h->c ? out_h->c + b0 : nullptr;
+            } else {
+                o.x = out_h->x ? out_h->x + int64_t(lo) * n_k * xs : nullptr;
+                o.c = out_h->c ? out_h->c + int64_t(lo) * n_k * xs : nullptr;
+            }
             rcs[r] = halda_solve_fleets_host(m->ctxs[size_t(r)], model, &sub, ks, n_k, &o);
             if (rcs[r] != HALDA_OK) errs[r] = g_err;
         });

@@ -4,7 +4,8 @@ Two modes:
 
 * throughput (`halda_solve_batch_distributed`, configs C3/C5): fleets are
   independent, so each rank solves a contiguous shard of them on its own GPU as
-  one halda_solve_fleets k-sweep (device-field table, no host lowering) — no
+  one halda_solve_fleets k-sweep (device-field table, no host lowering; the
+  objectives formed on the host in the reference's own arithmetic) — no
   collective on the data path; results are gathered once at the end.
 * latency (`halda_solve_distributed`, one fleet, config C2 at 8 GPUs): the
   k-candidates are dealt round-robin over the ranks, each rank solves its k's
@@ -128,12 +129,15 @@ def halda_solve_batch_distributed(fleets: Sequence[List[DeviceProfile]], model: 
     lo, hi = shard_bounds(len(fleets), rank, world)
     results: List[Optional[HALDAResult]] = []
     if _solve is None and hi > lo:
-        # the rank's shard as ONE GPU k-sweep (halda_solve_fleets: fused sweep from the device-field table)
-        from .solver.fleets import halda_solve_fleets
+        # the rank's shard as ONE GPU k-sweep (the fused sweep from the device-field table), objectives
+        # formed on the host exactly as the reference forms them (solver.halda._batch_on_gpu): the same
+        # obj_value, to the bit, as halda_solve of each fleet
+        from .solver.halda import _batch_on_gpu
+        from .solver.lower import kv_bits_to_factor
 
         dev = torch.cuda.current_device() if device is None else device
-        results = halda_solve_fleets(list(fleets[lo:hi]), model, k_candidates=Ks, mip_gap=mip_gap, kv_bits=kv_bits,
-                                     device=dev) if Ks else [None] * (hi - lo)
+        kv = kv_bits_to_factor(kv_bits)
+        results = _batch_on_gpu(list(fleets[lo:hi]), model, Ks, kv, dev) if Ks else [None] * (hi - lo)
     elif hi > lo:
         local = _solve(list(fleets[lo:hi]), model, Ks, kv_bits, mip_gap)
         for devs, per_k in zip(fleets[lo:hi], local):

@@ -18,6 +18,8 @@ import numpy as np
 
 LIB_PATH = Path(os.environ.get("HALDA_LIB", Path(__file__).resolve().parent.parent / "libhalda.so"))
 
+ABI_VERSION = 2  # include/halda.h HALDA_ABI_VERSION (2: halda_fleet_result.x_off)
+
 STATUS_OPTIMAL = 0
 STATUS_LIMIT = 1
 STATUS_INFEASIBLE = 2
@@ -96,6 +98,8 @@ def load_library(path: Path | str | None = None):
                                    "or `make -C distilp_amd/csrc`")
         lib = ctypes.CDLL(str(p))
         lib.halda_version.restype = ctypes.c_int
+        if lib.halda_version() != ABI_VERSION:
+            raise HaldaUnavailable(f"{p} has ABI {lib.halda_version()}, this binding needs {ABI_VERSION}: rebuild it")
         lib.halda_init.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         lib.halda_init.restype = ctypes.c_int
         lib.halda_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC), ctypes.POINTER(HaldaResultC)]
@@ -261,11 +265,12 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
-    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3}
+    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3, "seg": 4}
 
     def set_fleets_path(self, path) -> None:
-        """halda_solve_fleets on the fused sweep ("fused" / True, default: four fleets per wave where
-        they have at most 16 devices), the fused sweep one fleet per wave ("wave"), the CSR
+        """halda_solve_fleets on the fused sweep ("fused" / True, default: fleets of at most 16 devices
+        four per wave, one wave per open k -- the k-slot kernel), the same with the segment kernel
+        (four fleets per wave, every k in turn: "seg"), the fused sweep one fleet per wave ("wave"), the CSR
         pipeline ("csr" / False), or (test path) the fused sweep with every k = 1 solve of its
         register launch done by the exact DP it falls back to ("dp")."""
         code = self.FLEET_PATHS[path] if isinstance(path, str) else int(bool(path))
@@ -279,12 +284,13 @@ class HaldaContext:
 
     def last_fleet_ms(self) -> Dict[str, float]:
         """Device time of each launch of the last halda_solve_fleets call (zero entries dropped)."""
-        ms = (ctypes.c_double * 8)()
+        ms = (ctypes.c_double * 9)()
         rc = self.lib.halda_last_fleet_ms(self.ctx, ms)
         if rc != 0:
             raise RuntimeError(f"halda_last_fleet_ms failed ({rc}): {last_error(self.lib)}")
         names = ("halda_sweep_kernel", "halda_sweep_tables_kernel", "halda_lower_kernel", "halda_screen_kernel",
-                 "halda_solve_k1_kernel", "halda_solve_kernel", "halda_pick_kernel", "halda_sweep_seg_kernel")
+                 "halda_solve_k1_kernel", "halda_solve_kernel", "halda_pick_kernel", "halda_sweep_seg_kernel",
+                 "halda_sweep_kslot_kernel")
         return {n: float(v) for n, v in zip(names, ms) if v > 0.0}
 
     def last_phase_ms(self) -> Dict[str, float]:

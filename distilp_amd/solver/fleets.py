@@ -58,7 +58,7 @@ class HaldaFleetsC(ctypes.Structure):
 class HaldaFleetResultC(ctypes.Structure):
     _fields_ = [("best_k", ctypes.c_void_p), ("obj_value", ctypes.c_void_p), ("w", ctypes.c_void_p),
                 ("n", ctypes.c_void_p), ("obj_by_k", ctypes.c_void_p), ("status", ctypes.c_void_p),
-                ("x", ctypes.c_void_p), ("c", ctypes.c_void_p)]
+                ("x", ctypes.c_void_p), ("c", ctypes.c_void_p), ("x_off", ctypes.c_void_p)]
 
 
 def _bind(lib):
@@ -133,6 +133,13 @@ class FleetTable:
     def sizes(self) -> np.ndarray:
         return np.diff(self.dev_off)
 
+    def __setattr__(self, name, value):
+        # a packed table's fields are rows of its _blocks, which _host_struct hands to libhalda
+        # directly: reassigning a field detaches it, so the blocks no longer describe the table
+        if name != "_blocks" and "_blocks" in self.__dict__:
+            del self.__dict__["_blocks"]
+        object.__setattr__(self, name, value)
+
     def sets(self, f: int):
         """{"M1", "M2", "M3"} index lists of fleet f (dense_common.py:149-167)."""
         cls = self.os_class[self.dev_off[f]:self.dev_off[f + 1]]
@@ -195,8 +202,8 @@ def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) 
     """Pack fleets (lists of DeviceProfile) into a FleetTable: one pass of the C packer over the
     devices into three field blocks (f64 [10][nd], int64 [6][nd], uint8 [2][nd]); the table's fields
     are rows of those blocks. Same values, flags and exceptions as fleet_table_py."""
-    if _PACKER is None:
-        raise ImportError("distilp_amd/solver/_fleetpack.so is not built (run __graft_entry__.build())")
+    if _PACKER is None:  # the C packer is not built for this interpreter: the Python packer (same table)
+        return fleet_table_py(fleets, model)
     fleets = fleets if isinstance(fleets, (list, tuple)) else list(fleets)
     nf = len(fleets)
     nd = sum(len(d) for d in fleets)
@@ -273,6 +280,73 @@ def fleet_table_py(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfil
     return t
 
 
+def _padded(table: "FleetTable", vals: np.ndarray, fill=0.0) -> np.ndarray:
+    """[n_fleets, max_devices] view of a per-device array, fleet rows in device order, `fill` past a
+    fleet's end (a reshape when every fleet has the same size)."""
+    sizes = table.sizes()
+    nf, mmax = table.n_fleets, int(sizes.max()) if table.n_fleets else 0
+    if nf and int(sizes.min()) == mmax and int(table.dev_off[0]) == 0:
+        return vals[:nf * mmax].reshape(nf, mmax)
+    j = np.arange(mmax)
+    idx = table.dev_off[:-1, None] + j[None, :]
+    ok = j[None, :] < sizes[:, None]
+    return np.where(ok, vals[np.where(ok, idx, 0)], fill)
+
+
+def fleet_constants(table: "FleetTable", model: ModelProfile):
+    """Per fleet (sum t_comm, sum xi, kappa): the constant part of obj_value, each in the reference's
+    own summation order (halda_p_solver.py:356-357: Python loops over the devices from 0; kappa
+    dense_common.py:211-230: the head's four terms, then the M1 devices' and then the M3 devices'
+    RAM-headroom terms in index order), as NumPy column sweeps over all fleets at once: every
+    fleet's running sum takes the same additions in the same order as the scalar loop (padding adds
+    +0.0, which leaves a sum that starts at +0.0 unchanged). The table's packer already raised the
+    reference's errors (zero s_disk / T_cpu, a missing b_1)."""
+    nf = table.n_fleets
+    tc = _padded(table, table.t_comm)
+    uma = (table.flags & DEV_UMA) != 0
+    xi_dev = (table.t_ram2vram + table.t_vram2ram) * np.where(uma, 0.0, 1.0)
+    xm = _padded(table, xi_dev)
+    t_sum = np.zeros(nf)
+    x_sum = np.zeros(nf)
+    for i in range(tc.shape[1]):
+        t_sum = t_sum + tc[:, i]
+        x_sum = x_sum + xm[:, i]
+    # kappa's head: the first is_head device of the fleet, else its first device
+    head_local = np.argmax(_padded(table, (table.flags & DEV_HEAD).astype(np.int64), fill=0) != 0, axis=1)
+    h = table.dev_off[:-1] + head_local
+    scpu, Tc, sd, hflag = table.scpu_b1[h], table.T_cpu[h], table.s_disk[h], table.flags[h]
+    has_fout = "b_1" in model.f_out
+    f_out = float(model.f_out["b_1"]) if has_fout else 0.0
+    rate = has_fout & ((hflag & DEV_CPU_RATE) != 0) & (scpu > 0.0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        total = np.where(rate, 0.0 + f_out / np.where(rate, scpu, 1.0), 0.0)
+    bin_, bout, V = float(model.b_in), float(model.b_out), float(model.V)
+    total = total + (bin_ / V + bout) / Tc
+    total = total + bin_ / (V * sd)
+    total = total + bout / sd
+    # tail: M1 devices then M3 devices, each in index order
+    cls = _padded(table, table.os_class.astype(np.int64), fill=0)
+    rank = np.where(cls == 1, 0, np.where(cls == 3, 1, 2))
+    order = np.argsort(rank * (cls.shape[1] + 1) + np.arange(cls.shape[1])[None, :], axis=1, kind="stable")
+    term = (table.c_cpu - table.d_avail_ram - table.swap).astype(np.float64) / table.s_disk
+    tm = np.take_along_axis(np.where(rank < 2, _padded(table, term), 0.0), order, axis=1)
+    tail = np.zeros(nf)
+    for i in range(tm.shape[1]):
+        tail = tail + tm[:, i]
+    return t_sum, x_sum, total + tail
+
+
+def open_x_offsets(table: "FleetTable", model: ModelProfile, ks: Sequence[int]) -> np.ndarray:
+    """Compact x / c layout (halda_fleet_result.x_off) of the instances that can be optimal: W = L // k
+    >= M_f (else sum lb(w) = M_f > W: infeasible) and W < 1e6; -1 elsewhere. [n_fleets * n_k]."""
+    sizes = table.sizes()
+    W = np.asarray([int(model.L) // int(k) for k in ks], np.int64)
+    open_ = (W[None, :] >= sizes[:, None]) & (W[None, :] < 1_000_000)
+    n = np.where(open_, 7 * sizes[:, None] + 1, 0).ravel()
+    off = np.cumsum(n) - n
+    return np.where(open_.ravel(), off, -1).astype(np.int64)
+
+
 @dataclass
 class FleetSolve:
     """Per fleet: best k (0 = none feasible), obj_value, w / n (device layout); per (fleet, k): obj, status."""
@@ -284,8 +358,9 @@ class FleetSolve:
     obj_by_k: np.ndarray  # [n_fleets, n_k]
     status: np.ndarray  # [n_fleets, n_k]
     ks: List[int]
-    x: Optional[np.ndarray] = None  # [n_fleets, n_k, 7 max_devices + 1] when requested
+    x: Optional[np.ndarray] = None  # [n_fleets, n_k, 7 max_devices + 1] when requested (want_x=True)
     c: Optional[np.ndarray] = None
+    x_off: Optional[np.ndarray] = None  # want_x="open": [n_fleets * n_k] offsets into the flat x / c
 
 
 def _fleets_struct(t: FleetTable, ptr) -> HaldaFleetsC:
@@ -340,6 +415,9 @@ class MultiDeviceContext:
         from ._libhalda import HaldaUnavailable, load_library
 
         self.lib = _bind(load_library())
+        import threading
+
+        self._lock = threading.Lock()  # the per-GPU contexts' staging buffers are not reentrant
         ords = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
         self.ctx = ctypes.c_void_p()
         rc = self.lib.halda_init_multi(len(devices), ords, ctypes.byref(self.ctx))
@@ -365,7 +443,8 @@ class MultiDeviceContext:
 def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
                 device: int = 0, want_x: bool = False, _multi: Optional["MultiDeviceContext"] = None) -> FleetSolve:
     """halda_solve_fleets_host on a host FleetTable (synchronous). want_x: also x and the lowered c
-    of every (fleet, k) (so the host can form obj_value exactly as the reference, with NumPy)."""
+    of every (fleet, k) (so the host can form obj_value exactly as the reference, with NumPy);
+    want_x="open": only of the instances that can be optimal (open_x_offsets), flat, with x_off."""
     ks = [int(k) for k in ks]
     if not ks:
         raise ValueError("no k-candidates")
@@ -376,23 +455,33 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
     fs, keep = _host_struct(table)
     nf, nd, nk = table.n_fleets, table.n_devices, len(ks)
     # results in two buffers (f64, int32) viewed per field: two pointer reads
-    xs = 7 * int(fs.max_devices) + 1 if want_x else 0
-    fbuf = np.zeros(nf + nf * nk + 2 * nf * nk * xs)
+    xsel = open_x_offsets(table, model, ks) if want_x == "open" else None
+    if xsel is not None:
+        ext = int(np.max(xsel + np.repeat(7 * table.sizes() + 1, nk), initial=0)) if (xsel >= 0).any() else 0
+        xs = 0
+    else:
+        xs = 7 * int(fs.max_devices) + 1 if want_x else 0
+        ext = nf * nk * xs
+    fbuf = np.zeros(nf + nf * nk + 2 * ext)
     ibuf = np.zeros(nf + 2 * nd + nf * nk, np.int32)
     pf, pi = fbuf.ctypes.data, ibuf.ctypes.data
     o1, o2 = nf, nf + nf * nk
     out = FleetSolve(best_k=ibuf[:nf], obj_value=fbuf[:nf], w=ibuf[nf:nf + nd], n=ibuf[nf + nd:nf + 2 * nd],
                      obj_by_k=fbuf[o1:o2].reshape(nf, nk), status=ibuf[nf + 2 * nd:].reshape(nf, nk), ks=ks)
-    if want_x:
-        out.x = fbuf[o2:o2 + nf * nk * xs].reshape(nf, nk, xs)
-        out.c = fbuf[o2 + nf * nk * xs:].reshape(nf, nk, xs)
+    if xsel is not None:
+        out.x, out.c, out.x_off = fbuf[o2:o2 + ext], fbuf[o2 + ext:], xsel
+    elif want_x:
+        out.x = fbuf[o2:o2 + ext].reshape(nf, nk, xs)
+        out.c = fbuf[o2 + ext:].reshape(nf, nk, xs)
     r = HaldaFleetResultC(pi, pf, pi + 4 * nf, pi + 4 * (nf + nd), pf + 8 * o1, pi + 4 * (nf + 2 * nd),
-                          pf + 8 * o2 if want_x else None, pf + 8 * (o2 + nf * nk * xs) if want_x else None)
+                          pf + 8 * o2 if want_x else None, pf + 8 * (o2 + ext) if want_x else None,
+                          xsel.ctypes.data if xsel is not None else None)
     karr = np.asarray(ks, np.int32)
     m = model_struct(model, kv_factor)
     if _multi is not None:
-        rc = lib.halda_solve_fleets_multi(_multi.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
-                                          ctypes.byref(r))
+        with _multi._lock:
+                rc = lib.halda_solve_fleets_multi(_multi.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,
+                                              ctypes.byref(r))
     else:
         with ctx._lock:
             rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(fs), karr.ctypes.data, nk,

@@ -18,8 +18,9 @@ k-candidate is lowered on the GPU (bit-identical CSR to lower.lower_fleet, the
 host restatement pinned to the reference's arrays) and solved exactly (gap 0)
 in ONE halda_solve_fleets call, instead of one scipy/HiGHS call per k. The
 objective of each k is then formed here with NumPy from the returned c and x,
-exactly as the reference forms it. `halda_solve_batch` keeps the host lowering
-(one CSR per fleet shared by its k-instances through the C-ABI halda_solve_batch).
+exactly as the reference forms it. `halda_solve_batch` runs many fleets through ONE such call and
+forms every objective on the host the same way (vectorised offsets, one NumPy dot per feasible
+(fleet, k)).
 """
 
 from __future__ import annotations
@@ -29,35 +30,14 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..common import DeviceProfile, ModelProfile
-from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL, BatchResult, get_context
-from .batch import assemble
+from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL
 from .coefficients import HALDAResult, ILPResult, assign_sets, kappa_constant, valid_factors_of_L
 from .fleets import fleet_table, solve_table
-from .lower import FleetMILP, kv_bits_to_factor, lower_fleet
+from .lower import kv_bits_to_factor
 
 
 def _k_list(model: ModelProfile, k_candidates: Optional[Iterable[int]]) -> List[int]:
     return sorted(set(k_candidates)) if k_candidates else valid_factors_of_L(model.L)
-
-
-def _results_for(fleets: Sequence[FleetMILP], refs, res: BatchResult) -> List[List[Tuple[int, Optional[ILPResult]]]]:
-    """Per fleet: [(k, ILPResult or None if infeasible)] in k order."""
-    out: List[List[Tuple[int, Optional[ILPResult]]]] = [[] for _ in fleets]
-    for idx, ref in enumerate(refs):
-        fl = fleets[ref.fleet]
-        st = int(res.status[idx])
-        if st == STATUS_OPTIMAL:
-            x = res.x[ref.col_off:ref.col_off + ref.n_cols]
-            M = fl.M
-            w = [int(round(v)) for v in x[:M]]
-            n = [int(round(v)) for v in x[M:2 * M]]
-            out[ref.fleet].append((ref.k, ILPResult(k=ref.k, w=w, n=n, obj_value=fl.objective_value(ref.c, x))))
-        elif st == STATUS_INFEASIBLE:
-            out[ref.fleet].append((ref.k, None))
-        else:
-            raise RuntimeError(f"libhalda rejected instance (fleet {ref.fleet}, k={ref.k}) with status {st}: "
-                               "the lowered MILP does not have the HALDA structure")
-    return out
 
 
 def _offset_parts(devs, model: ModelProfile, sets) -> Tuple[float, float, float]:
@@ -160,6 +140,70 @@ def halda_solve(
     return result
 
 
+def _batch_on_gpu(fleets: Sequence[List[DeviceProfile]], model: ModelProfile, Ks: List[int], kv_factor: float,
+                  device: int, _multi=None) -> List[Optional[HALDAResult]]:
+    """Many fleets' k-sweeps in ONE halda_solve_fleets call (the fused sweep from the packed
+    device-field table), with every objective formed here exactly as the reference forms it
+    (halda_p_solver.py:347-357): per feasible (fleet, k), c.x with NumPy on the returned c and x
+    (only the instances with L // k >= M come back: open_x_offsets) -- np.vecdot over the rows of one
+    length runs numpy's 1-D dot loop per row, the bits of `float(c.dot(x))` -- + sum t_comm + sum xi +
+    kappa in the reference's own order (fleets.fleet_constants); best k by ascending k and strict "<"
+    (:407, the first minimum); w, n = int(round(x)) of the winner. None where no k is feasible."""
+    from .fleets import fleet_constants
+
+    if any(k == 0 for k in Ks):
+        raise ZeroDivisionError("integer division or modulo by zero")  # W = L // k (halda_p_solver.py:72)
+    fleets = fleets if isinstance(fleets, list) else list(fleets)
+    if not fleets:
+        return []
+    pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
+    table = fleet_table(fleets, model)
+    if not pos:
+        return [None] * len(fleets)
+    res = solve_table(table, model, pos, kv_factor, device, want_x="open", _multi=_multi)
+    st = res.status
+    bad = (st != STATUS_OPTIMAL) & (st != STATUS_INFEASIBLE)
+    if bad.any():
+        f, j = map(int, np.argwhere(bad)[0])
+        raise RuntimeError(f"libhalda rejected the (fleet {f}, k={pos[j]}) MILP with status {int(st[f, j])}: "
+                           "the lowered MILP does not have the HALDA structure")
+    t_sum, x_sum, kappa = fleet_constants(table, model)
+    nf, nk = table.n_fleets, len(pos)
+    sizes = table.sizes()
+    opt = st == STATUS_OPTIMAL
+    obj = np.full((nf, nk), np.inf)
+    xo = res.x_off.reshape(nf, nk)
+    for M in np.unique(sizes):  # one vectorised dot per row length N = 7 M + 1
+        N = 7 * int(M) + 1
+        fi, ji = np.nonzero(opt & (sizes == M)[:, None])
+        if len(fi) == 0:
+            continue
+        idx = xo[fi, ji][:, None] + np.arange(N)[None, :]
+        cx = np.vecdot(res.c[idx], res.x[idx])
+        obj[fi, ji] = ((cx + t_sum[fi]) + x_sum[fi]) + kappa[fi]
+    feas = opt.any(axis=1)
+    bj = np.argmin(obj, axis=1)  # the first minimum: ascending k, strict "<"
+    best_obj = obj[np.arange(nf), bj]
+    best_a = xo[np.arange(nf), bj]
+    out: List[Optional[HALDAResult]] = [None] * nf
+    cls = table.os_class
+    for M in np.unique(sizes):
+        M = int(M)
+        fs = np.flatnonzero(feas & (sizes == M))
+        if len(fs) == 0:
+            continue
+        wn = np.rint(res.x[best_a[fs][:, None] + np.arange(2 * M)[None, :]]).astype(np.int64).tolist()
+        cm = cls[table.dev_off[fs][:, None] + np.arange(M)[None, :]]
+        sets = {s: [r.tolist() for r in np.split(np.nonzero(cm == s)[1], np.cumsum((cm == s).sum(axis=1))[:-1])]
+                for s in (1, 2, 3)}
+        ks_f, ob_f = [pos[j] for j in bj[fs].tolist()], best_obj[fs].tolist()
+        for q, f in enumerate(fs.tolist()):
+            row = wn[q]
+            out[f] = HALDAResult.model_construct(w=row[:M], n=row[M:], k=ks_f[q], obj_value=ob_f[q],
+                                                 sets={"M1": sets[1][q], "M2": sets[2][q], "M3": sets[3][q]})
+    return out
+
+
 def halda_solve_batch(
     fleets: Sequence[List[DeviceProfile]],
     model: ModelProfile,
@@ -168,7 +212,8 @@ def halda_solve_batch(
     kv_bits: str = "8bit",
     device: int = 0,
 ) -> List[Optional[HALDAResult]]:
-    """Throughput API: many fleets (same model) in one GPU batch.
+    """Throughput API: many fleets (same model) in ONE GPU k-sweep (halda_solve_fleets, the fused
+    sweep), objectives formed on the host exactly as the reference forms them.
 
     Returns one HALDAResult per fleet, or None where no k is feasible (where
     `halda_solve` would raise). Prints nothing."""
@@ -178,17 +223,6 @@ def halda_solve_batch(
         L = model.L
         Ks = sorted({d for d in range(1, L) if L % d == 0}) if L > 1 else []
     kv_factor = kv_bits_to_factor(kv_bits)
-    lowered, sets_all = [], []
-    for devs in fleets:
-        sets = assign_sets(devs)
-        sets_all.append(sets)
-        lowered.append(lower_fleet(devs, model, kv_factor=kv_factor, sets=sets))
-    batch, refs = assemble(lowered, [Ks] * len(lowered), mip_gap)
-    res = get_context(device).solve(batch)
-    out: List[Optional[HALDAResult]] = []
-    for per_k, sets in zip(_results_for(lowered, refs, res), sets_all):
-        best = _pick(per_k)
-        out.append(None if best is None else HALDAResult(w=list(best.w), n=list(best.n), k=best.k,
-                                                         obj_value=best.obj_value,
-                                                         sets={k: list(v) for k, v in sets.items()}))
-    return out
+    if not Ks:
+        return [None] * len(fleets)
+    return _batch_on_gpu(fleets, model, Ks, kv_factor, device)

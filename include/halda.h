@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HALDA_ABI_VERSION 1
+#define HALDA_ABI_VERSION 2
 
 /* per-instance status (halda_result.status) */
 #define HALDA_STATUS_OPTIMAL 0       /* res.success == True                   */
@@ -186,6 +186,11 @@ typedef struct halda_fleet_result {
     int32_t *status;     /* [n_fleets * n_k] HALDA_STATUS_* per k; may be NULL */
     double *x;           /* [n_fleets * n_k * (7 max_devices + 1)] x per (fleet, k), column layout; may be NULL */
     double *c;           /* same layout: the lowered objective c per (fleet, k); may be NULL */
+    /* Optional compact x / c layout (ABI 2): x_off[f * n_k + j] = element offset of instance (f, k_j)'s
+     * 7 M_f + 1 entries in x and c, or -1 for an instance whose x / c are not wanted (e.g. L / k < M_f,
+     * which cannot be optimal). NULL: the dense layout above. Device memory for halda_solve_fleets,
+     * host memory for halda_solve_fleets_host / _multi (x and c then hold max(x_off + 7 M_f + 1)). */
+    const int64_t *x_off;
 } halda_fleet_result;
 
 /* Asynchronous on `stream` (NULL = the context's stream): the halda_fleets and
@@ -198,17 +203,21 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
 /* How halda_solve_fleets runs (default 1; HALDA_FLEETS_PATH=csr / =wave at halda_init select 0 / 2):
  * 1 the fused sweep (halda_sweep_kernel: every (fleet, k) built in registers from the device
  *   fields, solved and compared in one wave per fleet; no MILP is materialised); batches of more
- *   than 64 fleets of at most 16 devices (and at most 16 k) that need k > 1 tables run four fleets
- *   per wave (halda_sweep_seg_kernel, one per 16-lane segment);
+ *   than 64 fleets of at most 16 devices that need k > 1 tables run four fleets per wave, one per
+ *   16-lane segment, and one wave per open k (halda_sweep_kslot_kernel: the best k picked in the
+ *   workgroup), or, when its LDS does not fit (and at most 16 k), every k in turn in one wave
+ *   (halda_sweep_seg_kernel);
  * 2 the fused sweep, one fleet per wave only;
+ * 4 the fused sweep with the segment kernel instead of the k-slot kernel;
  * 0 the CSR pipeline (lowering kernel -> the halda_solve_batch kernels -> pick kernel), which also
  *   keeps the lowered batch for halda_last_lowered. All give the same statuses, x and k.
  * HALDA_E_ARG for any other path. */
 int halda_set_fleets_path(void *ctx, int path);
 
 /* Device time of the last halda_solve_fleets call per launch, in ms (per-launch events on, see
- * halda_set_timing; 0 for launches that did not run): ms8[0] the fused sweep kernel
- * (halda_sweep_kernel), ms8[7] the segment kernel (halda_sweep_seg_kernel), ms8[1] their table launch (halda_sweep_tables_kernel / halda_sweep_big_kernel:
+ * halda_set_timing; 0 for launches that did not run; ms8 holds 9 entries): ms8[0] the fused sweep kernel
+ * (halda_sweep_kernel), ms8[7] the segment kernel (halda_sweep_seg_kernel), ms8[8] the k-slot kernel
+ * (halda_sweep_kslot_kernel), ms8[1] their table launch (halda_sweep_tables_kernel / halda_sweep_big_kernel:
  * the flagged fleets, or the whole batch when k > 1 / wide fleets need tables from the start);
  * CSR pipeline: ms8[2] lowering, ms8[3] screen, ms8[4] k = 1 solve, ms8[5] general kernel,
  * ms8[6] pick. */

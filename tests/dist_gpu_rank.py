@@ -18,12 +18,13 @@ def main():
 
     from distilp_amd.common import ModelProfileSplit
     from distilp_amd.distributed import halda_solve_batch_distributed, halda_solve_distributed
+    from distilp_amd.solver import halda_solve
     from distilp_amd.synth import load_model_dict
     from tests.helpers import fixture_fleet, synth_devices
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = {"single": {}, "batch": {}}
+        out = {"single": {}, "batch": {}, "single_of_batch": {}}
         for folder, kv in (("llama_3_70b/online", "4bit"), ("hermes_70b", "4bit"), ("llama_3_70b/online", "8bit")):
             devs, model = fixture_fleet(folder)
             r = halda_solve_distributed(devs, model, mip_gap=1e-4, kv_bits=kv, device=0)
@@ -33,6 +34,10 @@ def main():
             fleets = [synth_devices(M, s) for s in range(20 if M < 64 else 8)]
             res = halda_solve_batch_distributed(fleets, m2, mip_gap=1e-4, kv_bits="4bit", device=0)
             out["batch"][str(M)] = [o.model_dump() for o in res]
+            # the same fleets one at a time through halda_solve (the objective must be the same bits)
+            out["single_of_batch"][str(M)] = [
+                halda_solve(devs, m2, mip_gap=1e-4, plot=False, kv_bits="4bit", device=0).model_dump()
+                for devs in fleets]
         with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
             json.dump(out, f)
     finally:

@@ -158,3 +158,29 @@ def test_host_zero_copy_x_of_infeasible_k_are_zero(llama_online_model):
         assert np.array_equal(big.status[:n], small.status)
         assert np.array_equal(big.x[:n, :, :N], small.x[:, :, :N]) and np.array_equal(big.c[:n, :, :N], small.c[:, :, :N])
     assert ctx is not None
+
+
+def test_batch_api_equals_halda_solve_bits(llama_online_model):
+    """halda_solve_batch (ONE fused k-sweep over all fleets, the objectives formed on the host from the
+    compact x / c of the open instances) returns exactly what halda_solve returns fleet by fleet --
+    k, w, n, sets and obj_value to the bit (the reference's own formula, halda_p_solver.py:347-357) --
+    on a ragged batch (1..64 devices, incl. the C2 shape's four feasible k) and on a uniform one."""
+    import contextlib
+    import io
+
+    from distilp_amd.solver import halda_solve
+
+    sizes = [1, 2, 5, 16, 16, 64, 3, 40, 16, 7] * 3
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(4200 + s, M)] for s, M in enumerate(sizes)]
+    for batch in (fleets, fleets[3:5] * 40):
+        out = halda_solve_batch(batch, llama_online_model, mip_gap=1e-4, kv_bits="4bit")
+        for devs, r in zip(batch, out):
+            with contextlib.redirect_stdout(io.StringIO()):
+                want = halda_solve(devs, llama_online_model, mip_gap=1e-4, plot=False, kv_bits="4bit")
+            assert r is not None
+            assert (r.k, r.w, r.n, r.sets, r.obj_value) == (want.k, want.w, want.n, want.sets, want.obj_value)
+    # user k lists: a negative k is infeasible, k = 0 raises like the reference's W = L // k
+    out = halda_solve_batch(fleets[:4], llama_online_model, k_candidates=[-2, 1, 3], kv_bits="4bit")
+    assert all(r is not None and r.k in (1, 3) for r in out)
+    with pytest.raises(ZeroDivisionError):
+        halda_solve_batch(fleets[:2], llama_online_model, k_candidates=[0, 1], kv_bits="4bit")

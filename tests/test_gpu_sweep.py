@@ -107,25 +107,32 @@ def test_multi_device_context_equals_single(llama_online_model):
         assert np.array_equal(one.x[fi, :, :N], many.x[fi, :, :N]) and np.array_equal(one.c[fi, :, :N], many.c[fi, :, :N])
 
 
-def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model):
-    """halda_sweep_seg_kernel (four fleets of <= 16 devices per wave) against the one-fleet-per-wave
-    sweep on 300 fleets of 1..16 devices: the same bits everywhere (statuses, obj_by_k, x, c, best k,
-    obj_value, w, n). One-device fleets and k = 1 fast-path fallbacks are flagged by the segment
-    kernel and redone by the gated table launch; the CSR pipeline agrees too."""
+@pytest.mark.parametrize("path,kernel,sizes", [
+    ("fused", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
+    ("fused", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
+    ("seg", "halda_sweep_seg_kernel", [1 + (s * 7) % 16 for s in range(300)]),
+])
+def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model, path, kernel, sizes):
+    """The two kernels for fleets of <= 16 devices -- halda_sweep_kslot_kernel (four fleets per wave,
+    one wave per open k, the best k picked in the workgroup; the default) and halda_sweep_seg_kernel
+    (four fleets per wave, every k in turn) -- against the one-fleet-per-wave sweep on fleets of 1..16
+    devices (and a C2-like batch of 16- and 12-device fleets): the same bits everywhere (statuses,
+    obj_by_k, x, c, best k, obj_value, w, n). One-device fleets and k = 1 fast-path fallbacks are
+    flagged and redone by the gated table launch; the CSR pipeline agrees too."""
     ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
-    sizes = [1 + (s * 7) % 16 for s in range(300)]
     fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(11000 + s, M)] for s, M in enumerate(sizes)]
     table = fleet_table(fleets, llama_online_model)
     ctx = get_context(0)
-    seg = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
     ctx.set_timing(True)
     try:
+        ctx.set_fleets_path(path)
+        seg = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
         solve_table(table, llama_online_model, ks, 0.5)
-        assert "halda_sweep_seg_kernel" in ctx.last_fleet_ms()  # the segment launch ran
+        assert kernel in ctx.last_fleet_ms()  # the segment / k-slot launch ran
         ctx.set_fleets_path("wave")
         wave = solve_table(table, llama_online_model, ks, 0.5, want_x=True)
         solve_table(table, llama_online_model, ks, 0.5)
-        assert "halda_sweep_seg_kernel" not in ctx.last_fleet_ms()
+        assert kernel not in ctx.last_fleet_ms()
     finally:
         ctx.set_fleets_path("fused")
         ctx.set_timing(False)
@@ -134,6 +141,20 @@ def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model):
     for fi, M in enumerate(sizes):
         N = 7 * M + 1
         assert np.array_equal(seg.x[fi, :, :N], wave.x[fi, :, :N]) and np.array_equal(seg.c[fi, :, :N], wave.c[fi, :, :N])
+    ctx.set_fleets_path(path)
+    try:  # the compact x / c layout (x_off) gives the same x / c of every open instance
+        op = solve_table(table, llama_online_model, ks, 0.5, want_x="open")
+    finally:
+        ctx.set_fleets_path("fused")
+    xo = op.x_off.reshape(len(sizes), len(ks))
+    for fi, M in enumerate(sizes):
+        N = 7 * M + 1
+        for j in range(len(ks)):
+            if xo[fi, j] >= 0:
+                a = xo[fi, j]
+                assert np.array_equal(op.x[a:a + N], wave.x[fi, j, :N]) and np.array_equal(op.c[a:a + N], wave.c[fi, j, :N])
+            else:
+                assert wave.status[fi, j] != 0
     ctx.set_fleets_path("csr")
     try:
         csr = solve_table(table, llama_online_model, ks, 0.5, want_x=True)

@@ -151,11 +151,18 @@ def test_c_packer_equals_python_packer(llama_online_model):
     import numpy as np
 
     from distilp_amd.common import DeviceProfile
-    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, fleet_table_py
+    from distilp_amd.solver import fleets as fleets_mod
+    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, _host_struct, fleet_table, fleet_table_py
     from distilp_amd.synth import synth_fleet
 
+    assert fleets_mod._PACKER is not None, "the C packer is not built for this interpreter"
     fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(500 + s, 1 + (s * 7) % 70)] for s in range(300)]
     a, b = fleet_table(fleets, llama_online_model), fleet_table_py(fleets, llama_online_model)
+    # a field reassigned on a packed table is what the C struct points at (the blocks are dropped)
+    t = fleet_table(fleets[:3], llama_online_model)
+    t.T_cpu = t.T_cpu * 2
+    s, keep = _host_struct(t)
+    assert not hasattr(t, "_blocks") and s.T_cpu == keep["T_cpu"].ctypes.data
     for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS:
         assert getattr(a, f).dtype == getattr(b, f).dtype and np.array_equal(getattr(a, f), getattr(b, f)), f
 
@@ -195,3 +202,67 @@ def test_bench_gpus_mismatch_fails_loudly():
                        text=True, timeout=120)
     assert p.returncode == 2 and "--gpus 2 but the launcher started 1 rank" in p.stderr
     assert p.stdout.strip() == ""
+
+
+def test_fleet_constants_equal_reference_order(llama_online_model):
+    """fleets.fleet_constants (NumPy column sweeps over all fleets) == the reference-order scalar loops
+    (halda._offset_parts: sum t_comm, sum xi, kappa of dense_common.py:211-230) bit for bit, on ragged
+    fleets with android swap, unified memory, no head and a head that is not device 0."""
+    import numpy as np
+
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.solver.coefficients import assign_sets
+    from distilp_amd.solver.fleets import fleet_constants, fleet_table
+    from distilp_amd.solver.halda import _offset_parts
+    from distilp_amd.synth import synth_fleet
+
+    fleets = []
+    for s in range(120):
+        devs = [DeviceProfile.model_validate(d) for d in synth_fleet(700 + s, 1 + (s * 11) % 67)]
+        if s % 5 == 1:
+            devs = [d.model_copy(update={"is_head": False}) for d in devs]
+        if s % 5 == 2 and len(devs) > 2:
+            devs = [d.model_copy(update={"is_head": i == 2}) for i, d in enumerate(devs)]
+        if s % 7 == 3:
+            devs = [d.model_copy(update={"os_type": "android", "d_bytes_can_swap": 3 << 30,
+                                         "d_swap_avail": 1 << 30}) if i % 2 else d for i, d in enumerate(devs)]
+        if s % 4 == 0:
+            devs = [d.model_copy(update={"is_unified_mem": True}) if i % 3 == 0 else d for i, d in enumerate(devs)]
+        fleets.append(devs)
+    t = fleet_table(fleets, llama_online_model)
+    ts, xs, ks = fleet_constants(t, llama_online_model)
+    for f, devs in enumerate(fleets):
+        want = _offset_parts(devs, llama_online_model, assign_sets(devs))
+        assert (ts[f], xs[f], ks[f]) == want, f
+    # a uniform batch takes the reshape path
+    same = fleets[7:8] * 5
+    t2 = fleet_table(same, llama_online_model)
+    want = _offset_parts(same[0], llama_online_model, assign_sets(same[0]))
+    assert all(tuple(v[f] for v in fleet_constants(t2, llama_online_model)) == want for f in range(5))
+    assert np.all(np.isfinite(ks))
+
+
+def test_open_x_offsets_layout(llama_online_model):
+    """Compact x / c layout: only instances with W = L // k >= M (and W < 1e6) get a slot, slots are
+    contiguous in (fleet, k) order, each 7 M + 1 long."""
+    import numpy as np
+
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.solver.fleets import fleet_table, open_x_offsets
+    from distilp_amd.synth import synth_fleet
+
+    sizes = [1, 16, 64, 3, 40]
+    t = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(s, m)] for s, m in enumerate(sizes)],
+                    llama_online_model)
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    off = open_x_offsets(t, llama_online_model, ks).reshape(len(sizes), len(ks))
+    nxt = 0
+    for f, M in enumerate(sizes):
+        for j, k in enumerate(ks):
+            if 80 // k >= M:
+                assert off[f, j] == nxt
+                nxt += 7 * M + 1
+            else:
+                assert off[f, j] == -1
+    assert (off >= 0).sum() == sum(sum(80 // k >= M for k in ks) for M in sizes)
+    assert np.array_equal(open_x_offsets(t, llama_online_model, []), np.zeros(0, np.int64))
