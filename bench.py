@@ -379,6 +379,30 @@ def time_to_optimal(model, M: int, runs: int = 100):
     return statistics.median(times)
 
 
+def batch_api(model, fleets, runs: int = 3):
+    """The public throughput API end to end: halda_solve_batch on the C3 fleets (a list of 4096
+    DeviceProfile lists -> 4096 HALDAResult): packing, ONE fused k-sweep (PCIe in / out), the host-formed
+    objectives. Median wall time of `runs` calls; the answers checked against one halda_solve."""
+    import contextlib
+    import io
+
+    from distilp_amd.solver import halda_solve, halda_solve_batch
+
+    times = []
+    out = None
+    for _ in range(runs + 1):
+        t0 = time.perf_counter()
+        out = halda_solve_batch(fleets, model, mip_gap=1e-4, kv_bits="4bit")
+        times.append((time.perf_counter() - t0) * 1e3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        one = halda_solve(fleets[0], model, mip_gap=1e-4, plot=False, kv_bits="4bit")
+    if (out[0].k, out[0].w, out[0].n, out[0].obj_value) != (one.k, one.w, one.n, one.obj_value):
+        raise RuntimeError("halda_solve_batch disagrees with halda_solve")
+    return {"what": f"halda_solve_batch on {len(fleets)} C3 fleets (DeviceProfile lists -> HALDAResult, host-formed "
+                    "objectives), median of the warm calls", "ms": statistics.median(times[1:]),
+            "fleets_per_s": len(fleets) / (statistics.median(times[1:]) * 1e-3)}
+
+
 def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
     """Config C5 (BASELINE.json configs[4]) end to end from the host: a base fleet (seed 0) re-profiled
     per instance (every numeric device field x LU(0.9, 1.1), FleetTable.perturbed), batches of B
@@ -644,6 +668,7 @@ def main():
     if rank == 0:
         tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
+        bapi = batch_api(model, fleets) if (world == 1 and not args.no_tto) else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -689,6 +714,7 @@ def main():
             },
             "c2": c2,
             "c5_stream": c5,
+            "batch_api": bapi,
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,
         }

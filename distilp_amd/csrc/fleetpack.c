@@ -14,8 +14,12 @@
  *   raises what fleets.fleet_table_py raises, FleetTable.check's ZeroDivisionErrors included
  */
 #define PY_SSIZE_T_CLEAN
+#define _GNU_SOURCE
 #include <Python.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 enum { HEAD = 1, UMA = 2, CPU_RATE = 4, GPU = 8, GPU_RATE = 16, CUDA_OK = 32, METAL_OK = 64, METAL_AVAIL = 128 };
@@ -25,7 +29,7 @@ enum { HEAD = 1, UMA = 2, CPU_RATE = 4, GPU = 8, GPU_RATE = 16, CUDA_OK = 32, ME
     X(sgpu_cuda) X(T_metal) X(T_cuda) X(d_avail_cuda) X(d_avail_metal) X(T_cpu) X(t_kvcpy_cpu) X(t_kvcpy_gpu) \
     X(t_ram2vram) X(t_vram2ram) X(t_comm) X(s_disk) X(d_avail_ram) X(c_cpu) X(c_gpu) X(d_bytes_can_swap) \
     X(d_swap_avail) X(b_1)
-#define DECL(n) static PyObject *k_##n;
+#define DECL(n) static PyObject *k_##n; static Py_hash_t h_##n;
 KEYS(DECL)
 #undef DECL
 
@@ -68,6 +72,211 @@ static int rate(PyObject *table, PyObject *Q, int fq, int *present, double *v) {
     return as_f64(b1, v);
 }
 
+/* ---------------------------------------------------------------- parallel pass
+ * Large tables are packed by several threads while the calling thread holds the GIL and waits, so
+ * no Python code runs and no object changes meanwhile. The workers only READ: borrowed instance
+ * dicts (_PyObject_GetDictPtr), lookups by precomputed hash in str-keyed dicts
+ * (_PyDict_GetItem_KnownHash: no error state, no Python code), and the values of exact float / int /
+ * bool / None / str / dict objects. No reference count changes, no allocation, no exception: any
+ * value outside that (a missing key, another type, an overflow, a FLOPs table without "b_1") makes the
+ * worker give up, and the whole table is packed again by the serial pass below, which raises the
+ * reference's exceptions in the reference's order. So the parallel pass either writes exactly what
+ * the serial one would, or nothing that is kept. */
+typedef struct {
+    PyObject **devs;
+    Py_ssize_t lo, hi, nd;
+    PyObject *Q;
+    Py_hash_t hQ;
+    int fq;
+    double *f64;
+    int64_t *i64;
+    uint8_t *cls, *flg;
+    volatile int *bail;
+} Job;
+
+static PyObject *fget(PyObject *d, PyObject *k, Py_hash_t h) { return _PyDict_GetItem_KnownHash(d, k, h); }
+#define FGET(d, name) fget(d, k_##name, h_##name)
+
+static int fbool(PyObject *o, int *t) {
+    if (o == Py_True) *t = 1;
+    else if (o == Py_False) *t = 0;
+    else return -1;
+    return 0;
+}
+static int fdict(PyObject *o) { return o && PyDict_CheckExact(o) && _PyDict_HasOnlyStringKeys(o); }
+static int ff64(PyObject *o, double *v) {
+    if (!o || !PyFloat_CheckExact(o)) return -1;
+    *v = PyFloat_AS_DOUBLE(o);
+    return 0;
+}
+static int fi64(PyObject *o, int64_t *v) {
+    if (!o || !PyLong_CheckExact(o)) return -1;
+    int ovf = 0;
+    const long long x = PyLong_AsLongLongAndOverflow(o, &ovf);
+    if (ovf) return -1; /* an exact int never sets an error here */
+    *v = (int64_t)x;
+    return 0;
+}
+/* "table" truthy: a non-empty exact dict (None / empty: 0); anything else: -1 */
+static int ftable(PyObject *o) {
+    if (o == Py_None) return 0;
+    if (!fdict(o)) return -1;
+    return PyDict_GET_SIZE(o) > 0;
+}
+/* a load-throughput value: None / 0.0 falsy, a float truthy; anything else -1 */
+static int fthru(PyObject *o) {
+    if (o == Py_None) return 0;
+    if (!PyFloat_CheckExact(o)) return -1;
+    return PyFloat_AS_DOUBLE(o) != 0.0;
+}
+
+/* one device, the serial pass's reads restricted to the plain cases; -1: give up */
+static int fast_dev(const Job *J, PyObject *obj, Py_ssize_t g) {
+    PyObject **dp = _PyObject_GetDictPtr(obj);
+    if (!dp || !fdict(*dp)) return -1;
+    PyObject *d = *dp, *o;
+    PyObject *os = FGET(d, os_type);
+    if (!os || !PyUnicode_CheckExact(os)) return -1;
+    int c = 3;
+    if (PyUnicode_CompareWithASCIIString(os, "mac_no_metal") == 0) c = 1;
+    else if (PyUnicode_CompareWithASCIIString(os, "mac_metal") == 0) c = 2;
+    const int android = PyUnicode_CompareWithASCIIString(os, "android") == 0;
+    int fl = 0, t;
+    if (!(o = FGET(d, is_head)) || fbool(o, &t)) return -1;
+    fl |= t ? HEAD : 0;
+    if (!(o = FGET(d, is_unified_mem)) || fbool(o, &t)) return -1;
+    fl |= t ? UMA : 0;
+    PyObject *sc = FGET(d, scpu);
+    if (!sc) return -1;
+    double v = 0.0;
+    const int st = ftable(sc);
+    if (st < 0) return -1;
+    if (st) {
+        PyObject *row = _PyDict_GetItem_KnownHash(sc, J->Q, J->hQ);
+        if (row && row != Py_None) {
+            if (!fdict(row)) return -1;
+            PyObject *b1 = FGET(row, b_1);
+            if (!b1 || ff64(b1, &v)) return -1; /* b_1 missing: the serial pass decides whether it raises */
+            fl |= CPU_RATE;
+        }
+    }
+    PyObject *hm = FGET(d, has_metal), *hc = FGET(d, has_cuda);
+    int has_metal, has_cuda;
+    if (!hm || !hc || fbool(hm, &has_metal) || fbool(hc, &has_cuda)) return -1;
+    PyObject *sm = FGET(d, sgpu_metal), *scu = FGET(d, sgpu_cuda), *tm = FGET(d, T_metal), *tcu = FGET(d, T_cuda);
+    if (!sm || !scu || !tm || !tcu) return -1;
+    const int tsm = ftable(sm), tsc = ftable(scu), ttm = fthru(tm), ttc = fthru(tcu);
+    if (tsm < 0 || tsc < 0 || ttm < 0 || ttc < 0) return -1;
+    PyObject *table = (has_metal && tsm) ? sm : (has_cuda && tsc) ? scu : NULL;
+    PyObject *tg = (has_metal && ttm) ? tm : (has_cuda && ttc) ? tcu : NULL;
+    double gv = 0.0, tgv = 1.0;
+    if (table && tg) {
+        fl |= GPU;
+        PyObject *row = _PyDict_GetItem_KnownHash(table, J->Q, J->hQ);
+        if (row) {
+            if (!fdict(row)) return -1;
+            PyObject *b1 = FGET(row, b_1);
+            if (!b1) {
+                if (J->fq) return -1;
+            } else {
+                if (ff64(b1, &gv)) return -1;
+                fl |= GPU_RATE;
+            }
+        }
+        if (ff64(tg, &tgv)) return -1;
+    }
+    PyObject *dc = FGET(d, d_avail_cuda), *dm = FGET(d, d_avail_metal);
+    if (!dc || !dm) return -1;
+    if (has_cuda && dc != Py_None) fl |= CUDA_OK;
+    if (dm != Py_None) fl |= METAL_AVAIL | (has_metal ? METAL_OK : 0);
+    double fv[10];
+    fv[0] = v;
+    fv[1] = gv;
+    fv[3] = tgv;
+    if (ff64(FGET(d, T_cpu), &fv[2]) || ff64(FGET(d, t_kvcpy_cpu), &fv[4]) || ff64(FGET(d, t_kvcpy_gpu), &fv[5]) ||
+        ff64(FGET(d, t_ram2vram), &fv[6]) || ff64(FGET(d, t_vram2ram), &fv[7]) || ff64(FGET(d, t_comm), &fv[8]) ||
+        ff64(FGET(d, s_disk), &fv[9]))
+        return -1;
+    int64_t iv[6] = {0, 0, 0, 0, 0, 0};
+    if (fi64(FGET(d, d_avail_ram), &iv[0]) || fi64(FGET(d, c_cpu), &iv[1]) || fi64(FGET(d, c_gpu), &iv[2])) return -1;
+    if (dc != Py_None && fi64(dc, &iv[3])) return -1; /* dc or 0: an int's value either way */
+    if (dm != Py_None && fi64(dm, &iv[4])) return -1;
+    if (android) {
+        int64_t a1, a2;
+        if (fi64(FGET(d, d_bytes_can_swap), &a1) || fi64(FGET(d, d_swap_avail), &a2)) return -1;
+        iv[5] = a1 < a2 ? a1 : a2;
+    }
+    const Py_ssize_t nd = J->nd;
+    for (int a = 0; a < 10; ++a) J->f64[a * nd + g] = fv[a];
+    for (int a = 0; a < 6; ++a) J->i64[a * nd + g] = iv[a];
+    J->cls[g] = (uint8_t)c;
+    J->flg[g] = (uint8_t)fl;
+    return 0;
+}
+
+static void *worker(void *arg) {
+    const Job *J = (const Job *)arg;
+    for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g)
+        if (fast_dev(J, J->devs[g], g)) *J->bail = 1;
+    return NULL;
+}
+
+static int pack_threads(Py_ssize_t nd) {
+    const char *e = getenv("HALDA_PACK_THREADS");
+    if (e && *e) return atoi(e);
+    if (nd < 8192) return 1;
+    cpu_set_t cs;
+    int n = 1;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+    return n < 16 ? n : 16;
+}
+
+/* 1: packed in parallel; 0: not attempted / given up (the caller packs serially); -1: error set */
+static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f64, int64_t *i64, uint8_t *cls,
+                         int64_t *off, int64_t *heads, Py_ssize_t nd) {
+    (void)fout;
+    const Py_ssize_t nf = PySequence_Fast_GET_SIZE(seq);
+    int nt = pack_threads(nd);
+    if (nt < 1 || (nt == 1 && !getenv("HALDA_PACK_THREADS")) || !PyUnicode_CheckExact(Q)) return 0;
+    const Py_hash_t hQ = PyObject_Hash(Q);
+    if (hQ == -1) return -1;
+    PyObject **devs = (PyObject **)malloc(sizeof(PyObject *) * (size_t)(nd > 0 ? nd : 1));
+    if (!devs) return 0;
+    Py_ssize_t g = 0;
+    off[0] = 0;
+    for (Py_ssize_t f = 0; f < nf; ++f) {
+        PyObject *fl = PySequence_Fast_GET_ITEM(seq, f);
+        if (!PyList_CheckExact(fl) && !PyTuple_CheckExact(fl)) { free(devs); return 0; }
+        const Py_ssize_t M = PySequence_Fast_GET_SIZE(fl);
+        if (M == 0 || g + M > nd) { free(devs); return 0; }
+        PyObject **items = PySequence_Fast_ITEMS(fl);
+        for (Py_ssize_t i = 0; i < M; ++i) devs[g + i] = items[i];
+        g += M;
+        off[f + 1] = g;
+    }
+    if (g != nd) { free(devs); return 0; }
+    if (nt > 64) nt = 64;
+    pthread_t th[64];
+    Job jobs[64];
+    volatile int bail = 0;
+    int started = 0;
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (Job){devs, nd * t / nt, nd * (t + 1) / nt, nd, Q, hQ, fq, f64, i64, cls, cls + nd, &bail};
+        if (pthread_create(&th[t], NULL, worker, &jobs[t]) != 0) { bail = 1; break; }
+        ++started;
+    }
+    for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+    free(devs);
+    if (bail) return 0;
+    const uint8_t *flg = cls + nd;
+    for (Py_ssize_t f = 0; f < nf; ++f) { /* kappa's head: the first is_head device, else device 0 */
+        heads[f] = off[f];
+        for (Py_ssize_t j = off[f]; j < off[f + 1]; ++j)
+            if (flg[j] & HEAD) { heads[f] = j; break; }
+    }
+    return 1;
+}
+
 static PyObject *pack(PyObject *self, PyObject *args) {
     (void)self;
     PyObject *fleets, *Q;
@@ -86,6 +295,14 @@ static PyObject *pack(PyObject *self, PyObject *args) {
     int64_t *i64 = (int64_t *)bi.buf, *off = (int64_t *)bo.buf, *heads = (int64_t *)bh.buf;
     uint8_t *cls = (uint8_t *)bu.buf, *flg = cls + nd;
     Py_ssize_t g = 0;
+    {
+        const int par = pack_parallel(seq, Q, fq, fout, f64, i64, cls, off, heads, nd);
+        if (par < 0) goto done;
+        if (par == 1) {
+            g = nd;
+            goto checks;
+        }
+    }
     off[0] = 0;
     for (Py_ssize_t f = 0; f < nf; ++f) {
         PyObject *devs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, f), "a fleet must be a sequence");
@@ -219,6 +436,7 @@ static PyObject *pack(PyObject *self, PyObject *args) {
         PyErr_SetString(PyExc_ValueError, "pack: device count does not match the buffers");
         goto done;
     }
+checks:
     /* FleetTable.check: the reference's ZeroDivisionErrors (alpha: b' / T_cpu; kappa: the head's
      * s_disk and every M1 / M3 device's), after the whole table is packed as there */
     for (Py_ssize_t j = 0; j < nd; ++j) {
@@ -245,13 +463,77 @@ done:
     return ret;
 }
 
+/* consts(f64, i64, u8, off, heads, fout, f_out_b1, b_in, b_out, V, out) -> None
+ * Per fleet of a packed table, the constant part of obj_value in the reference's own order
+ * (halda_p_solver.py:356-357, dense_common.py:211-230): out[0][f] = sum t_comm and out[1][f] = sum xi
+ * over the devices from the first (Python's `s = 0; for d in devs: s += ...`), out[2][f] = kappa: the
+ * head's four terms, then the M1 devices' and then the M3 devices' RAM-headroom terms in index order.
+ * IEEE double arithmetic in that order (built with -ffp-contract=off): the bits of the Python loops. */
+static PyObject *consts(PyObject *self, PyObject *args) {
+    (void)self;
+    Py_buffer bf, bi, bu, bo, bh, bout;
+    int fout;
+    double f_out_b1, b_in, b_out, V;
+    if (!PyArg_ParseTuple(args, "y*y*y*y*y*pddddw*", &bf, &bi, &bu, &bo, &bh, &fout, &f_out_b1, &b_in, &b_out, &V,
+                          &bout))
+        return NULL;
+    PyObject *ret = NULL;
+    const Py_ssize_t nd = bu.len / 2, nf = bh.len / 8;
+    if (bf.len < 80 * nd || bi.len < 48 * nd || bo.len < 8 * (nf + 1) || bout.len < 24 * nf) {
+        PyErr_SetString(PyExc_ValueError, "consts: buffers too small");
+        goto done;
+    }
+    {
+        const double *f64 = (const double *)bf.buf;
+        const int64_t *i64 = (const int64_t *)bi.buf, *off = (const int64_t *)bo.buf, *heads = (const int64_t *)bh.buf;
+        const uint8_t *cls = (const uint8_t *)bu.buf, *flg = cls + nd;
+        const double *scpu = f64, *Tc = f64 + 2 * nd, *r2v = f64 + 6 * nd, *v2r = f64 + 7 * nd, *tcomm = f64 + 8 * nd,
+                     *sd = f64 + 9 * nd;
+        const int64_t *ram = i64, *ccpu = i64 + nd, *swap = i64 + 5 * nd;
+        double *out = (double *)bout.buf;
+        for (Py_ssize_t f = 0; f < nf; ++f) {
+            const int64_t a = off[f], b = off[f + 1], h = heads[f];
+            if (a < 0 || b > nd || a > b || h < a || h >= b) {
+                PyErr_SetString(PyExc_ValueError, "consts: bad offsets");
+                goto done;
+            }
+            double t = 0.0, x = 0.0;
+            for (int64_t j = a; j < b; ++j) t += tcomm[j];
+            for (int64_t j = a; j < b; ++j) x += (r2v[j] + v2r[j]) * ((flg[j] & UMA) ? 0.0 : 1.0);
+            double total = 0.0;
+            if (fout && (flg[h] & CPU_RATE)) total = scpu[h] > 0.0 ? 0.0 + f_out_b1 / scpu[h] : 0.0;
+            total += (b_in / V + b_out) / Tc[h];
+            total += b_in / (V * sd[h]);
+            total += b_out / sd[h];
+            double tail = 0.0;
+            for (int pass = 1; pass <= 3; pass += 2)
+                for (int64_t j = a; j < b; ++j)
+                    if (cls[j] == pass) tail += (double)(ccpu[j] - ram[j] - swap[j]) / sd[j];
+            out[f] = t;
+            out[nf + f] = x;
+            out[2 * nf + f] = total + tail;
+        }
+    }
+    Py_INCREF(Py_None);
+    ret = Py_None;
+done:
+    PyBuffer_Release(&bf);
+    PyBuffer_Release(&bi);
+    PyBuffer_Release(&bu);
+    PyBuffer_Release(&bo);
+    PyBuffer_Release(&bh);
+    PyBuffer_Release(&bout);
+    return ret;
+}
+
 static PyMethodDef methods[] = {{"pack", pack, METH_VARARGS, "Pack fleets of DeviceProfile into the fleet table."},
+                                {"consts", consts, METH_VARARGS, "Per-fleet obj_value constants of a packed table."},
                                 {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_fleetpack", NULL, -1, methods, NULL, NULL, NULL, NULL};
 
 PyMODINIT_FUNC PyInit__fleetpack(void) {
-#define MAKE(n) if (!(k_##n = PyUnicode_InternFromString(#n))) return NULL;
+#define MAKE(n) if (!(k_##n = PyUnicode_InternFromString(#n)) || (h_##n = PyObject_Hash(k_##n)) == -1) return NULL;
     KEYS(MAKE)
 #undef MAKE
     return PyModule_Create(&mod);

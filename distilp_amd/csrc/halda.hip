@@ -27,6 +27,7 @@
 // Floating point keeps the reference's operation order (-ffp-contract=off).
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -4045,6 +4046,8 @@ struct Ctx {
     bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
     bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
     bool last_fleet_fused = false;
+    void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
+    size_t shard_bytes = 0;
     void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
     size_t fflag_bytes = 0;
     hipStream_t last_stream = nullptr;
@@ -4424,6 +4427,58 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     return HALDA_OK;
 }
 
+// ---------------------------------------------------------------- latency mode over RCCL
+// One process per GPU, the ranks of an RCCL communicator: rank r sweeps the k-candidates
+// ks[r], ks[r + world], ... of every fleet (halda_sweep_* on its own GPU), then the ranks agree on each
+// fleet's best k with the reference's rule -- the smallest obj_value, ties to the smallest k
+// (halda_p_solver.py:407) -- by three all-reduces over xGMI: MIN of obj_value, MIN of the k that
+// reaches it, SUM of (w, n) where only the owner of that k contributes (the ranks' k's are disjoint),
+// plus MIN / MAX of the per-k objectives / statuses when requested. Kernels between them turn one
+// reduction's output into the next one's input on the device; nothing returns to the host.
+__global__ __launch_bounds__(64) void halda_shard_kernel(int mode, int n_k, int n_sub, int rank, int world,
+                                                         const int64_t *dev_off, halda_fleet_result sub,
+                                                         halda_fleet_result out) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int64_t d0 = dev_off[f], d1 = dev_off[f + 1];
+    if (mode == 0) {  // local results into the full layout, neutral elements elsewhere
+        if (lane == 0) out.obj_value[f] = n_sub > 0 ? sub.obj_value[f] : kInf;
+        for (int64_t d = d0 + lane; d < d1; d += 64) {
+            out.w[d] = n_sub > 0 ? sub.w[d] : 0;
+            out.n[d] = n_sub > 0 ? sub.n[d] : 0;
+        }
+        for (int j = lane; j < n_k; j += 64) {
+            const bool own = j % world == rank;
+            const int js = j / world;
+            if (out.obj_by_k) out.obj_by_k[int64_t(f) * n_k + j] = own ? sub.obj_by_k[int64_t(f) * n_sub + js] : kInf;
+            if (out.status) out.status[int64_t(f) * n_k + j] = own ? sub.status[int64_t(f) * n_sub + js] : INT32_MIN;
+        }
+    } else if (mode == 1) {  // after MIN(obj_value): the k this rank offers for the global minimum
+        if (lane == 0) {
+            const int bk = n_sub > 0 ? sub.best_k[f] : 0;
+            out.best_k[f] = bk > 0 && sub.obj_value[f] == out.obj_value[f] ? bk : INT32_MAX;
+        }
+    } else {  // after MIN(k): only the owner keeps its (w, n) for the SUM
+        const int bk = n_sub > 0 ? sub.best_k[f] : 0;
+        const int kmin = out.best_k[f];
+        if (bk != kmin || kmin == INT32_MAX)
+            for (int64_t d = d0 + lane; d < d1; d += 64) out.w[d] = out.n[d] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void halda_shard_final_kernel(int nf, halda_fleet_result out) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f < nf && out.best_k[f] == INT32_MAX) out.best_k[f] = 0;  // no rank has a feasible k
+}
+
+int nccl_fail(ncclResult_t r, const char *what) {
+    return fail(HALDA_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+#define NCCL_TRY(expr)                                     \
+    do {                                                   \
+        ncclResult_t r_ = (expr);                          \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #expr); \
+    } while (0)
+
 }  // namespace
 
 extern "C" {
@@ -4494,6 +4549,7 @@ void halda_free(void *ctx) {
     if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
     if (c->gtab) (void)hipFree(c->gtab);
     if (c->fflag) (void)hipFree(c->fflag);
+    if (c->shard) (void)hipFree(c->shard);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_host) (void)hipEventDestroy(c->ev_host);
     if (c->evf0) (void)hipEventDestroy(c->evf0);
@@ -4989,6 +5045,107 @@ int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_f
     for (auto &t : th) t.join();
     for (int r = 0; r < nd; ++r)
         if (rcs[r] != HALDA_OK) return fail(rcs[r], "device " + std::to_string(r) + ": " + errs[r]);
+    return HALDA_OK;
+}
+
+int halda_comm_unique_id(void *id128) {
+    if (!id128) return fail(HALDA_E_ARG, "NULL id");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id128, &id, sizeof(id));
+    return HALDA_OK;
+}
+
+int halda_comm_init(void **comm, int world, int rank, const void *id128, int device_ordinal) {
+    if (!comm || !id128 || world < 1 || rank < 0 || rank >= world) return fail(HALDA_E_ARG, "halda_comm_init: bad arguments");
+    HIP_TRY(hipSetDevice(device_ordinal));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof(id));
+    ncclComm_t c = nullptr;
+    NCCL_TRY(ncclCommInitRank(&c, world, id, rank));
+    *comm = c;
+    return HALDA_OK;
+}
+
+void halda_comm_destroy(void *comm) {
+    if (comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm));
+}
+
+int halda_solve_fleets_sharded(void *ctx, void *comm, const halda_model *model, const halda_fleets *fleets,
+                               const int32_t *ks, int32_t n_k, halda_fleet_result *out, void *stream) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !comm || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL argument");
+    if (out->x || out->c) return fail(HALDA_E_ARG, "halda_solve_fleets_sharded: x / c are not gathered (pass NULL)");
+    if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
+    ncclComm_t cm = static_cast<ncclComm_t>(comm);
+    int world = 0, rank = 0;
+    NCCL_TRY(ncclCommCount(cm, &world));
+    NCCL_TRY(ncclCommUserRank(cm, &rank));
+    const halda_fleets &F = *fleets;
+    const int64_t nf = F.n_fleets;
+    if (nf <= 0) return HALDA_OK;
+    if (n_k <= 0 || n_k > 1024) return fail(HALDA_E_ARG, "n_k must be in 1..1024");
+    for (int j = 0; j < n_k; ++j)
+        if (ks[j] < 1 || (j && ks[j] <= ks[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    // this rank's k's: ks[rank], ks[rank + world], ... (halda_solve_distributed deals them the same way)
+    std::vector<int32_t> mine;
+    for (int j = rank; j < n_k; j += world) mine.push_back(ks[j]);
+    const int n_sub = int(mine.size());
+    // device count: nf * M for one fleet size, else read back from dev_off[nf] (a synchronous copy)
+    int64_t nd = nf * F.max_devices;
+    if (F.min_devices != F.max_devices) {
+        HIP_TRY(hipMemcpyAsync(&nd, F.dev_off + nf, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_bk = take(4 * nf), o_obj = take(8 * nf), o_w = take(4 * size_t(nd)), o_n = take(4 * size_t(nd)),
+                 o_obk = take(8 * nf * std::max(n_sub, 1)), o_st = take(4 * nf * std::max(n_sub, 1));
+    if (off > c->shard_bytes) {
+        if (c->shard) HIP_TRY(hipFree(c->shard));
+        c->shard = nullptr;
+        c->shard_bytes = 0;
+        HIP_TRY(hipMalloc(&c->shard, off));
+        c->shard_bytes = off;
+    }
+    char *base = static_cast<char *>(c->shard);
+    halda_fleet_result sub = {};
+    sub.best_k = reinterpret_cast<int32_t *>(base + o_bk);
+    sub.obj_value = reinterpret_cast<double *>(base + o_obj);
+    sub.w = reinterpret_cast<int32_t *>(base + o_w);
+    sub.n = reinterpret_cast<int32_t *>(base + o_n);
+    sub.obj_by_k = out->obj_by_k ? reinterpret_cast<double *>(base + o_obk) : nullptr;
+    sub.status = out->status ? reinterpret_cast<int32_t *>(base + o_st) : nullptr;
+    {
+        const int rc = order_after_previous(c, s);  // the shard scratch is per context
+        if (rc != HALDA_OK) return rc;
+    }
+    if (n_sub > 0) {
+        const int rc = halda_solve_fleets(ctx, model, fleets, mine.data(), n_sub, &sub, s);
+        if (rc != HALDA_OK) return rc;
+    }
+    const halda_fleet_result o = *out;
+    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 0, int(n_k), n_sub, rank, world,
+                       F.dev_off, sub, o);
+    HIP_TRY(hipGetLastError());
+    NCCL_TRY(ncclAllReduce(o.obj_value, o.obj_value, size_t(nf), ncclFloat64, ncclMin, cm, s));
+    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 1, int(n_k), n_sub, rank, world,
+                       F.dev_off, sub, o);
+    HIP_TRY(hipGetLastError());
+    NCCL_TRY(ncclAllReduce(o.best_k, o.best_k, size_t(nf), ncclInt32, ncclMin, cm, s));
+    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 2, int(n_k), n_sub, rank, world,
+                       F.dev_off, sub, o);
+    HIP_TRY(hipGetLastError());
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclAllReduce(o.w, o.w, size_t(nd), ncclInt32, ncclSum, cm, s));
+    NCCL_TRY(ncclAllReduce(o.n, o.n, size_t(nd), ncclInt32, ncclSum, cm, s));
+    if (o.obj_by_k) NCCL_TRY(ncclAllReduce(o.obj_by_k, o.obj_by_k, size_t(nf) * n_k, ncclFloat64, ncclMin, cm, s));
+    if (o.status) NCCL_TRY(ncclAllReduce(o.status, o.status, size_t(nf) * n_k, ncclInt32, ncclMax, cm, s));
+    NCCL_TRY(ncclGroupEnd());
+    hipLaunchKernelGGL(halda_shard_final_kernel, dim3(unsigned((nf + 255) / 256)), dim3(256), 0, s, int(nf), o);
+    HIP_TRY(hipGetLastError());
     return HALDA_OK;
 }
 

@@ -82,6 +82,17 @@ def _bind(lib):
     lib.halda_solve_fleets_multi.restype = ctypes.c_int
     lib.halda_free_multi.argtypes = [ctypes.c_void_p]
     lib.halda_free_multi.restype = None
+    lib.halda_comm_unique_id.argtypes = [ctypes.c_void_p]
+    lib.halda_comm_unique_id.restype = ctypes.c_int
+    lib.halda_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                    ctypes.c_int]
+    lib.halda_comm_init.restype = ctypes.c_int
+    lib.halda_comm_destroy.argtypes = [ctypes.c_void_p]
+    lib.halda_comm_destroy.restype = None
+    lib.halda_solve_fleets_sharded.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HaldaModelC),
+                                               ctypes.POINTER(HaldaFleetsC), ctypes.c_void_p, ctypes.c_int32,
+                                               ctypes.POINTER(HaldaFleetResultC), ctypes.c_void_p]
+    lib.halda_solve_fleets_sharded.restype = ctypes.c_int
     lib._fleets_bound = True
     return lib
 
@@ -136,8 +147,9 @@ class FleetTable:
     def __setattr__(self, name, value):
         # a packed table's fields are rows of its _blocks, which _host_struct hands to libhalda
         # directly: reassigning a field detaches it, so the blocks no longer describe the table
-        if name != "_blocks" and "_blocks" in self.__dict__:
+        if name not in ("_blocks", "_heads") and "_blocks" in self.__dict__:
             del self.__dict__["_blocks"]
+            self.__dict__.pop("_heads", None)
         object.__setattr__(self, name, value)
 
     def sets(self, f: int):
@@ -216,6 +228,7 @@ def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) 
     t = FleetTable(dev_off=off, os_class=u8[0], flags=u8[1], **{f: f64[j] for j, f in enumerate(F64_FIELDS)},
                    **{f: i64[j] for j, f in enumerate(I64_FIELDS)})
     t._blocks = (off, u8, f64, i64)  # FleetTable.check ran in the packer
+    t._heads = heads                   # kappa's head of each fleet (global device index)
     return t
 
 
@@ -294,6 +307,21 @@ def _padded(table: "FleetTable", vals: np.ndarray, fill=0.0) -> np.ndarray:
 
 
 def fleet_constants(table: "FleetTable", model: ModelProfile):
+    """Per fleet (sum t_comm, sum xi, kappa): the constant part of obj_value in the reference's own
+    order -- by the C packer's `consts` on a packed table (scalar loops, the bits of the reference's
+    Python loops), else by fleet_constants_np."""
+    blocks, heads = getattr(table, "_blocks", None), getattr(table, "_heads", None)
+    if _PACKER is None or blocks is None or heads is None or not hasattr(_PACKER, "consts"):
+        return fleet_constants_np(table, model)
+    off, u8, f64, i64 = blocks
+    out = np.empty((3, table.n_fleets))
+    fout = "b_1" in model.f_out
+    _PACKER.consts(f64, i64, u8, off, heads, fout, float(model.f_out["b_1"]) if fout else 0.0, float(model.b_in),
+                   float(model.b_out), float(model.V), out)
+    return out[0], out[1], out[2]
+
+
+def fleet_constants_np(table: "FleetTable", model: ModelProfile):
     """Per fleet (sum t_comm, sum xi, kappa): the constant part of obj_value, each in the reference's
     own summation order (halda_p_solver.py:356-357: Python loops over the devices from 0; kappa
     dense_common.py:211-230: the head's four terms, then the M1 devices' and then the M3 devices'
@@ -557,3 +585,45 @@ class DeviceFleetTable:
         if rc != 0:
             raise RuntimeError(f"halda_solve_fleets failed ({rc}): {last_error(lib)}")
 
+
+
+class RcclComm:
+    """An RCCL communicator owned by libhalda (halda_comm_init): one per rank, `world` ranks, the
+    128-byte id from `RcclComm.unique_id()` on one rank handed to the others by any channel."""
+
+    def __init__(self, world: int, rank: int, uid: bytes, device: int = 0):
+        from ._libhalda import HaldaUnavailable, load_library
+
+        self.lib = _bind(load_library())
+        self.comm = ctypes.c_void_p()
+        rc = self.lib.halda_comm_init(ctypes.byref(self.comm), world, rank, uid, device)
+        if rc != 0:
+            raise HaldaUnavailable(f"halda_comm_init failed ({rc}): {last_error(self.lib)}")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from ._libhalda import load_library
+
+        lib = _bind(load_library())
+        buf = ctypes.create_string_buffer(128)
+        rc = lib.halda_comm_unique_id(buf)
+        if rc != 0:
+            raise RuntimeError(f"halda_comm_unique_id failed ({rc}): {last_error(lib)}")
+        return buf.raw
+
+    def close(self):
+        if getattr(self, "comm", None):
+            self.lib.halda_comm_destroy(self.comm)
+            self.comm = None
+
+
+def launch_sharded(dt: "DeviceFleetTable", ctx, comm: RcclComm, stream: int) -> None:
+    """Latency mode over RCCL (halda_solve_fleets_sharded): this rank sweeps its share of dt's
+    k-candidates and the ranks all-reduce to the same best k / obj_value / w / n (and obj_by_k / status
+    when dt holds them) in dt.out, on every rank."""
+    lib = _bind(ctx.lib)
+    with ctx._lock:
+        rc = lib.halda_solve_fleets_sharded(ctx.ctx, comm.comm, ctypes.byref(dt.model), ctypes.byref(dt.fs),
+                                            dt.ks.ctypes.data, len(dt.ks), ctypes.byref(dt.res), ctypes.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"halda_solve_fleets_sharded failed ({rc}): {last_error(lib)}")

@@ -32,7 +32,7 @@ import numpy as np
 from ..common import DeviceProfile, ModelProfile
 from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL
 from .coefficients import HALDAResult, ILPResult, assign_sets, kappa_constant, valid_factors_of_L
-from .fleets import fleet_table, solve_table
+from .fleets import fleet_constants, fleet_table, solve_table
 from .lower import kv_bits_to_factor
 
 
@@ -63,8 +63,7 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
     W = L // k (:72), then the k-independent coefficient errors (b_1 missing, zero T_cpu / s_disk,
     empty fleet) at the first k, after that k's debug line."""
     try:
-        offsets = _offset_parts(devs, model, sets)
-        table = fleet_table([devs], model)
+        table = fleet_table([devs], model)  # the reference's coefficient / kappa errors, raised by the packer
         err = None
     except Exception as e:  # noqa: BLE001 -- re-raised at the first k, as the reference raises it
         err = e
@@ -83,6 +82,8 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
         if k > 0:
             if res is None:
                 res = solve_table(table, model, pos, kv_factor, device, want_x=True)
+                # sum t_comm, sum xi, kappa in the reference's order (the packer's C loops)
+                offsets = tuple(float(v[0]) for v in fleet_constants(table, model))
             j = pos.index(k)
             st = int(res.status[0, j])
             if st == STATUS_OPTIMAL:
@@ -149,8 +150,6 @@ def _batch_on_gpu(fleets: Sequence[List[DeviceProfile]], model: ModelProfile, Ks
     length runs numpy's 1-D dot loop per row, the bits of `float(c.dot(x))` -- + sum t_comm + sum xi +
     kappa in the reference's own order (fleets.fleet_constants); best k by ascending k and strict "<"
     (:407, the first minimum); w, n = int(round(x)) of the winner. None where no k is feasible."""
-    from .fleets import fleet_constants
-
     if any(k == 0 for k in Ks):
         raise ZeroDivisionError("integer division or modulo by zero")  # W = L // k (halda_p_solver.py:72)
     fleets = fleets if isinstance(fleets, list) else list(fleets)

@@ -238,6 +238,23 @@ int halda_solve_fleets_multi(void *mctx, const halda_model *model, const halda_f
                              int32_t n_k, halda_fleet_result *out);
 void halda_free_multi(void *mctx);
 
+/* Latency mode across processes, one per GPU: the ranks of an RCCL communicator
+ * (ncclComm_t, passed as void*) each sweep their share of the k-candidates of every fleet --
+ * ks[rank], ks[rank + world], ... -- on their own GPU (halda_solve_fleets), then agree on each fleet's
+ * best k by the reference's rule (smallest obj_value, ties to the smallest k, halda_p_solver.py:407)
+ * with device-side all-reduces over xGMI: MIN of obj_value, MIN of the k reaching it, SUM of the owner's
+ * (w, n), and MIN / MAX of obj_by_k / status when those are requested. Every rank ends with the same
+ * halda_fleet_result (device arrays; x and c must be NULL). Asynchronous on `stream`; every rank calls
+ * it with the same fleets and ks. obj_value is the GPU-formed objective (see halda_solve_fleets).
+ * halda_comm_unique_id / halda_comm_init / halda_comm_destroy wrap ncclGetUniqueId / ncclCommInitRank
+ * (the 128-byte id goes from one rank to the others by any channel) for callers without their own
+ * communicator. */
+int halda_comm_unique_id(void *id128);
+int halda_comm_init(void **comm, int world, int rank, const void *id128, int device_ordinal);
+void halda_comm_destroy(void *comm);
+int halda_solve_fleets_sharded(void *ctx, void *comm, const halda_model *model, const halda_fleets *fleets,
+                               const int32_t *ks, int32_t n_k, halda_fleet_result *out, void *stream);
+
 /* The lowered batch of the last halda_solve_fleets call (device pointers into ctx
  * scratch, valid until the next call on ctx): for tests and diagnostics. An
  * instance with L / k < M (bound-infeasible) carries only its header, w bounds,

@@ -55,3 +55,38 @@ def test_two_ranks_on_one_gpu_match_goldens(tmp_path, fixtures_golden, synth_gol
             assert _close(r["obj_value"], ref["obj_value"])
         # throughput mode forms obj_value on the host like halda_solve does: the same bits
         assert res == got["single_of_batch"][M], M
+
+
+def test_rccl_sharded_latency_mode_world_one():
+    """The C ABI's latency mode over RCCL (halda_solve_fleets_sharded) on a one-rank communicator
+    built by libhalda itself: the k-sharding bookkeeping, the three device-side all-reduces and the
+    scatter / owner kernels between them leave exactly the single-GPU sweep's results (best k,
+    obj_value, w, n, obj_by_k, status) on a C2-like and a ragged batch. (More ranks need more GPUs than
+    this box has: RCCL does not put two ranks on one device.)"""
+    import torch
+
+    from distilp_amd.common import DeviceProfile, ModelProfileSplit
+    from distilp_amd.solver._libhalda import get_context
+    from distilp_amd.solver.fleets import DeviceFleetTable, RcclComm, fleet_table, launch_sharded
+    from distilp_amd.synth import load_model_dict, synth_fleet
+
+    m2 = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    stream = torch.cuda.Stream(dev)
+    comm = RcclComm(1, 0, RcclComm.unique_id(), 0)
+    try:
+        for sizes in ([16] * 100, [1 + (s * 5) % 64 for s in range(80)]):
+            fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(3100 + s, M)] for s, M in enumerate(sizes)]
+            table = fleet_table(fleets, m2)
+            a = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+            b = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+            a.launch(ctx, stream.cuda_stream)
+            launch_sharded(b, ctx, comm, stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status"):
+                assert torch.equal(a.out[f], b.out[f]), f
+            assert (b.out["best_k"] > 0).all()
+    finally:
+        comm.close()

@@ -184,6 +184,32 @@ def test_c_packer_equals_python_packer(llama_online_model):
     ]
     for fl in cases:
         assert err(lambda: fleet_table(fl, m)) == err(lambda: fleet_table_py(fl, m)), fl
+    # the packer's parallel pass (several threads reading the profiles, forced on here by
+    # HALDA_PACK_THREADS; by default it runs from 8,192 devices): the same table, and the same
+    # exception through its serial fallback
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, '.');"
+        "from tests.conftest import *; from distilp_amd.common import DeviceProfile;"
+        "from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, fleet_table_py;"
+        "from distilp_amd.synth import synth_fleet, load_model_dict;"
+        "from distilp_amd.common import ModelProfileSplit;"
+        "m = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile();"
+        "fl = [[DeviceProfile.model_validate(d) for d in synth_fleet(900 + s, 1 + (s * 5) % 64)] for s in range(200)];"
+        "fl[7] = [d.model_copy(update={'os_type': 'android', 'd_bytes_can_swap': 7, 'd_swap_avail': 5}) for d in fl[7]];"
+        "a, b = fleet_table(fl, m), fleet_table_py(fl, m);"
+        "assert all(np.array_equal(getattr(a, f), getattr(b, f)) for f in ('dev_off', 'os_class', 'flags') + F64_FIELDS + I64_FIELDS);"
+        "bad = fl[:50] + [[fl[50][0].model_copy(update={'T_cpu': 0.0})] + fl[50][1:]];"
+        "e = None\ntry: fleet_table(bad, m)\nexcept ZeroDivisionError as x: e = x\nassert e is not None;"
+        "miss = fl[:9] + [[fl[9][0].model_copy(update={'scpu': {m.Q: {'b_2': 1.0}}})] + fl[9][1:]];"
+        "e = None\ntry: fleet_table(miss, m)\nexcept ValueError as x: e = x\nassert 'b_1' in str(e);"
+        "print('ok')")
+    env = dict(__import__("os").environ, HALDA_PACK_THREADS="4")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=str(__import__("pathlib").Path(__file__).resolve().parent.parent))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
     ok = fleet_table(cases[-1], m)
     assert np.array_equal(ok.swap, fleet_table_py(cases[-1], m).swap) and (ok.swap == 5).all()
 
@@ -212,7 +238,7 @@ def test_fleet_constants_equal_reference_order(llama_online_model):
 
     from distilp_amd.common import DeviceProfile
     from distilp_amd.solver.coefficients import assign_sets
-    from distilp_amd.solver.fleets import fleet_constants, fleet_table
+    from distilp_amd.solver.fleets import fleet_constants, fleet_constants_np, fleet_table
     from distilp_amd.solver.halda import _offset_parts
     from distilp_amd.synth import synth_fleet
 
@@ -230,10 +256,13 @@ def test_fleet_constants_equal_reference_order(llama_online_model):
             devs = [d.model_copy(update={"is_unified_mem": True}) if i % 3 == 0 else d for i, d in enumerate(devs)]
         fleets.append(devs)
     t = fleet_table(fleets, llama_online_model)
+    assert hasattr(t, "_heads")  # the C packer's table: fleet_constants runs its C loops
     ts, xs, ks = fleet_constants(t, llama_online_model)
+    tn, xn, kn = fleet_constants_np(t, llama_online_model)
     for f, devs in enumerate(fleets):
         want = _offset_parts(devs, llama_online_model, assign_sets(devs))
         assert (ts[f], xs[f], ks[f]) == want, f
+        assert (tn[f], xn[f], kn[f]) == want, f
     # a uniform batch takes the reshape path
     same = fleets[7:8] * 5
     t2 = fleet_table(same, llama_online_model)
