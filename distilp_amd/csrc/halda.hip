@@ -84,6 +84,13 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
     } while (0)
 #define HALDA_TSTAMP(slot) do {} while (0)
 #endif
+// k-slot kernel: per (workgroup, slot) wave, slots 0..4 shader clock (start, records done, solved,
+// after the barrier, pick done), 5 the constant-rate clock at start
+#define HALDA_KSTAMPW(slot, v)                                                                          \
+    do {                                                                                                \
+        const int64_t e_ = int64_t(blockIdx.x) * SA.n_slot + q;                                         \
+        if ((threadIdx.x & 63) == 0 && e_ < kStampInst) g_halda_stamps[e_ * kStamps + (slot)] = (v);    \
+    } while (0)
 #elif defined(HALDA_MARKS)  // asm listing only: phase markers for tools/asm_regions.py
 #define HALDA_SSTAMP(slot, v) asm volatile("; PHASE_MARK " #slot)
 #define HALDA_TSTAMP(slot) do {} while (0)
@@ -100,6 +107,9 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 #define HALDA_STAMP(k) \
     do {               \
     } while (0)
+#endif
+#ifndef HALDA_KSTAMPW
+#define HALDA_KSTAMPW(slot, v) do {} while (0)
 #endif
 // -DHALDA_STAMPS_DECODE: stamps 1..5 mark the round trips inside decode_k1 instead
 #ifdef HALDA_STAMPS_DECODE
@@ -3173,12 +3183,27 @@ __device__ inline void opaque_rec(FieldRec &r) {
 // Kernel arguments. Everything a wave reads through the scalar cache comes first (six 64-B lines:
 // the model, the table pointers, the result pointers, the counts); the k list, which lanes read
 // with vector loads, last.
+// halda_fleet_result without x_off (ABI 2's compact layout travels at the end of SweepArgs): the
+// result pointers stay within the kernel arguments' first lines, read through the scalar cache.
+struct FleetOut {
+    int32_t *best_k;
+    double *obj_value;
+    int32_t *w, *n;
+    double *obj_by_k;
+    int32_t *status;
+    double *x, *c;
+    FleetOut() = default;
+    __host__ __device__ FleetOut(const halda_fleet_result &r)
+        : best_k(r.best_k), obj_value(r.obj_value), w(r.w), n(r.n), obj_by_k(r.obj_by_k), status(r.status), x(r.x),
+          c(r.c) {}
+};
+
 struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
     int n_k;
     int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
-    halda_fleet_result out;
+    FleetOut out;
     int64_t xstride;
     uint8_t *fflag;  // per fleet: 1 = needs the table launch
     int *hb_flag;
@@ -3190,6 +3215,7 @@ struct SweepArgs {
     int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
     unsigned char *gtab;           // kGlobal: per-wave slices
     int64_t gstride;
+    const int64_t *x_off;          // halda_fleet_result.x_off (compact x / c layout) or nullptr
     int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
     int32_t Ws[64];  // W = L / k per k (host integer division)
 };
@@ -3199,7 +3225,7 @@ struct SweepArgs {
 // Element offset of instance inst's x / c: the dense layout, or the caller's compact x_off (-1: not
 // written).
 __device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
-    return A.out.x_off ? A.out.x_off[inst] : inst * A.xstride;
+    return A.x_off ? A.x_off[inst] : inst * A.xstride;
 }
 
 __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
@@ -3238,8 +3264,9 @@ __device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
 // tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
 // only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
 // the one-fleet-per-wave table launch, as the register-only launch does.
-template <bool kTables, bool kGlobal, class SG = Wave>
-__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg) {
+template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false>
+__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg, const DevFields &pre = {},
+                            int64_t pre_base = 0) {
     constexpr int S = SG::S;
     constexpr bool kSeg = S < 64;
     constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
@@ -3269,8 +3296,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         // fleet size the loads are issued at once from dev_off[0] = 0 (the usual table) while the
         // scalar read of dev_off[0] is in flight, and reissued only where it is not 0: no dependent
         // round trip in front of the field loads.
-        DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
-        if (A.uM > 0) {
+        // pre: the caller loaded this lane's fields already (the pipelined kernel, one fleet size, its
+        // dev_off[0] = pre_base applied)
+        DevFields mf;
+        if constexpr (kPre) mf = pre;
+        else mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        if constexpr (kPre) {
+            d0 += pre_base;
+        } else if (A.uM > 0) {
             // a vector read (returns in order behind the field loads: no wait of its own, unlike a
             // scalar read, whose lgkmcnt wait would also hold the kernel-argument reads)
             const int64_t base = __builtin_amdgcn_readfirstlane(int(F.dev_off[0])) |
@@ -3645,6 +3678,43 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
     sweep_fleet<false, false>(A, f, w, Wave(int(threadIdx.x & 63)));
 }
 
+// The register-only sweep, pipelined: a grid of nw waves (fewer than the fleets), wave w takes fleets
+// w, w + nw, w + 2 nw, ... and issues the field loads of its next fleet before it solves the current
+// one, so the next fleet's memory round trip hides behind this fleet's compute and the dispatcher
+// launches nw waves instead of one per fleet. One fleet size for the batch (uM <= 64), else the
+// one-fleet-per-wave kernel runs. The per-fleet work is sweep_fleet's, bit for bit.
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_pipe_kernel(
+    SweepArgs A, int nw) {
+    const int wv = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    {
+        const int nf = A.F.n_fleets, nk = A.n_k, um = A.uM;
+        const int64_t *doff = A.F.dev_off;
+        const double bp = A.Mo.b_prime;
+        const double *tc = A.F.T_cpu;
+        const int32_t *ow = A.out.w;
+        asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
+    }
+    const int nf = A.F.n_fleets;
+    if (wv >= nf) return;
+    const int lane = threadIdx.x & 63;
+    const int M = A.uM;
+    const int li = lane < M ? lane : 0;
+    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
+    WaveCtx w = {};
+    w.dparg = dparg[threadIdx.x >> 6];
+    // the first fleet's fields from dev_off[0] = 0 (the usual table), reloaded where it is not 0
+    DevFields nxt = load_fields(A.F, int64_t(wv) * M + li);
+    const int64_t base = __builtin_amdgcn_readfirstlane(int(A.F.dev_off[0])) |
+                         (int64_t(__builtin_amdgcn_readfirstlane(int(uint64_t(A.F.dev_off[0]) >> 32))) << 32);
+    if (base != 0) nxt = load_fields(A.F, base + int64_t(wv) * M + li);
+    for (int f = wv; f < nf; f += nw) {
+        const DevFields cur = nxt;
+        const int fn = f + nw;
+        if (fn < nf) nxt = load_fields(A.F, base + int64_t(fn) * M + li);  // in flight during this fleet
+        sweep_fleet<false, false, Wave, true>(A, f, w, Wave(lane), cur, base);
+    }
+}
+
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     sweep_body<true, false>(A, smem);
@@ -3725,7 +3795,7 @@ struct SlotArgs {
 // One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
 // its w / n candidate).
 __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tabcap, const WaveCtx &w,
-                            const Seg<kSegLanes> &sg, SlotPick *pk) {
+                            const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec) {
     using SG = Seg<kSegLanes>;
     constexpr int S = SG::S;
     const int lane = sg.sl;
@@ -3740,6 +3810,11 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
     double tsum, xsum, kappa;
     fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
     const bool anybad = sg.any(bad != 0);
+#ifdef HALDA_STAMPS
+    *t_rec = __builtin_amdgcn_s_memtime();
+#else
+    (void)t_rec;
+#endif
     const int k = A.ks[j], W = A.Ws[j];
     const int64_t inst = int64_t(f) * A.n_k + j;
     const double kc = double(k - 1);
@@ -3924,6 +3999,8 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     const int nf = A.F.n_fleets;
     const int64_t f = int64_t(blockIdx.x) * kPer + seg;
     SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
+    HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
+    HALDA_KSTAMPW(5, __builtin_amdgcn_s_memrealtime());
     {
         const int tab = SA.tab[q];
         const int64_t tb = align16(int64_t(tab) * 8);
@@ -3932,10 +4009,15 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         w.G = reinterpret_cast<double *>(base);
         w.H = reinterpret_cast<double *>(base + tb);
         w.st0 = reinterpret_cast<int *>(base + 2 * tb);
-        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q);
+        unsigned long long t_rec = 0;
+        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q, &t_rec);
+        HALDA_KSTAMPW(1, t_rec);
     }
+    HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
     __syncthreads();
+    HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
     if (q == 0 && f < nf) kslot_pick(A, SA, int(f), pick + seg * SA.n_slot, sg);
+    HALDA_KSTAMPW(4, __builtin_amdgcn_s_memtime());
 }
 
 // halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
@@ -4040,6 +4122,7 @@ struct Ctx {
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
+    int sweep_waves = 0;                         // > 0: the register launch as the pipelined kernel, this many waves
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
@@ -4328,7 +4411,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         A.Ws[j] = kh[j] != 0 ? model.L / kh[j] : 0;
     }
     A.n_k = n_k;
-    A.out = out;
+    A.out = FleetOut(out);
+    A.x_off = out.x_off;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
     A.fflag = scratch ? static_cast<uint8_t *>(c->fflag) + 256 : nullptr;
     A.hb_flag = c->hb_flag;
@@ -4381,8 +4465,15 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipGetLastError());
     } else {
         A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
-                           dim3(64 * kSweepWavesPerBlock), 0, s, A);
+        const int pipe_waves = c->sweep_waves > 0 && A.uM > 0 && A.uM <= kK1MaxM && nf > c->sweep_waves ? c->sweep_waves : 0;
+        if (pipe_waves > 0) {
+            hipLaunchKernelGGL(halda_sweep_pipe_kernel,
+                               dim3(unsigned((pipe_waves + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
+                               dim3(64 * kSweepWavesPerBlock), 0, s, A, pipe_waves);
+        } else {
+            hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
+                               dim3(64 * kSweepWavesPerBlock), 0, s, A);
+        }
         HIP_TRY(hipGetLastError());
         if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;  // the fleets flagged above, gated on the hand-back flag
@@ -4522,6 +4613,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
+    const char *sw = std::getenv("HALDA_SWEEP_WAVES");
+    c->sweep_waves = sw ? std::atoi(sw) : 0;
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
