@@ -1,0 +1,1620 @@
+// halda_sweep.hpp -- the whole k-sweep (halda_solve_fleets): the GPU lowering, the fused sweep kernels
+// (register, pipelined, table, segment, k-slot) and the CSR path's pick kernel.
+// Part of libhalda's single translation unit: included by halda.hip inside its anonymous namespace
+// (after halda_solve.hpp); not a standalone header.
+#pragma once
+// ---------------------------------------------------------------- GPU lowering
+// halda_lower_kernel: one wave per fleet, lane = device, writes the fleet's
+// fixed-k MILPs for every k-candidate into the halda_batch layout with fixed
+// per-fleet strides (solve kernels read them unchanged). Restates the host
+// lowering (distilp_amd/solver/lower.py, itself the reference's
+// solve_fixed_k_milp, halda_p_solver.py:59-338, with dense_common.py:25-230):
+// same row order, same zero-dropping, same FP operation order -> the same CSR
+// and vectors bit for bit. An instance with W = L / k < M (every device needs a
+// layer: bound-infeasible, 8 of the 9 k at M = 64, L = 80) gets only what the
+// screen settles it from: header, w bounds, c[C] and the equality row's bounds.
+struct LowerDims {
+    int mmax, n_k;
+    int64_t cols, rows, nnz;  // strides per instance (cols, rows) and per fleet (nnz)
+};
+
+__host__ __device__ inline LowerDims lower_dims(int mmax, int n_k) {
+    LowerDims d;
+    d.mmax = mmax;
+    d.n_k = n_k;
+    d.cols = 7 * int64_t(mmax) + 1;
+    d.rows = 6 * int64_t(mmax) + 1;   // link M, capacity <= M, VRAM <= 2M, cycle 2M, equality 1
+    d.nnz = 26 * int64_t(mmax);       // 2M + 3M + 4M + 16M + M
+    return d;
+}
+
+// Exclusive prefix sum over the wave (all lanes active); total in *tot.
+__device__ inline int wave_excl_scan(int v, int lane, int *tot) {
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    *tot = __shfl(x, 63);
+    return x - v;
+}
+
+// sum_f_over_s (dense_common.py:49-75) for a key/quantisation known present or absent.
+__device__ inline double f_over_s(bool present, double f, double s) {
+    return present ? (s > 0.0 ? 0.0 + f / s : 0.0) : 0.0;
+}
+
+// Per-device coefficients of the fixed-k MILP (dense_common.py:25-126 and the penalties of
+// halda_p_solver.py:195-224) in the reference's operation order; shared by the lowering kernel
+// (CSR out) and the sweep kernel (records straight into registers), so both see the same bits.
+struct DevCoef {
+    double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+};
+
+// One device's table entry in registers: every field loaded unconditionally (one memory round
+// trip for all of them), the coefficients computed from the registers.
+struct DevFields {
+    double scpu, sgpu, Tc, Tg, tkc, tkg, r2v, v2r, tcomm, sdisk;
+    int64_t ram, ccpu, cgpu, cuda, metal, swap;
+    int cls, flags;
+};
+
+__device__ inline DevFields load_fields(const halda_fleets &F, int64_t g) {
+    DevFields f;
+    f.scpu = F.scpu_b1[g]; f.sgpu = F.sgpu_b1[g]; f.Tc = F.T_cpu[g]; f.Tg = F.T_gpu[g];
+    f.tkc = F.t_kvcpy_cpu[g]; f.tkg = F.t_kvcpy_gpu[g]; f.r2v = F.t_ram2vram[g]; f.v2r = F.t_vram2ram[g];
+    f.tcomm = F.t_comm[g]; f.sdisk = F.s_disk[g];
+    f.ram = F.d_avail_ram[g]; f.ccpu = F.c_cpu[g]; f.cgpu = F.c_gpu[g]; f.cuda = F.d_avail_cuda[g];
+    f.metal = F.d_avail_metal[g]; f.swap = F.swap[g];
+    f.cls = F.os_class[g];
+    f.flags = F.flags[g];
+    return f;
+}
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) {
+    DevCoef o;
+    const double bp = Mo.b_prime;
+    const int fl = F.flags;
+    const int cls = F.cls;
+    const double Tc = F.Tc, tkc = F.tkc, tkg = F.tkg;
+    const double cpu = f_over_s(Mo.has_f_q && (fl & HALDA_DEV_CPU_RATE), Mo.f_q_b1, F.scpu);
+    const bool hb = fl & HALDA_DEV_GPU;
+    const double gpu = hb ? f_over_s(Mo.has_f_q && (fl & HALDA_DEV_GPU_RATE), Mo.f_q_b1, F.sgpu) : 0.0;
+    const double tg = hb ? F.Tg : 1.0;
+    o.alpha = (cpu + tkc) + (bp / Tc);
+    const double beta = hb ? ((gpu - cpu) + (tkg - tkc)) + (bp / tg - bp / Tc) : 0.0;
+    o.b = cls == 1 ? 0.0 : beta;
+    o.xi = (F.r2v + F.v2r) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
+    const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+    o.bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.ccpu);
+    const double sd = fmax(1.0, F.sdisk);
+    o.p_bp = bp / sd;
+    o.p_b = Mo.b_layer / sd;
+    o.p_v = cls == 2 ? o.p_b : o.p_bp;
+    o.cst = o.xi + F.tcomm;
+    return o;
+}
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    return dev_coef(Mo, load_fields(F, g));
+}
+
+// Right-hand sides of the capacity rows (halda_p_solver.py:227-277).
+__device__ inline double rhs_ram(const DevFields &F, int set, double bcio) {
+    if (set == 1) return double(F.ram) - bcio;
+    if (set == 2) return double(F.metal) - bcio - double(F.cgpu);
+    return double(F.ram + F.swap) - bcio;
+}
+__device__ inline double rhs_cuda(const DevFields &F) { return double(F.cuda) - double(F.cgpu); }
+__device__ inline double rhs_metal(const halda_model &Mo, const DevFields &F) {
+    const double head = (F.flags & HALDA_DEV_HEAD) ? 1.0 : 0.0;
+    return double(F.metal) - double(F.cgpu) - Mo.b_out * head;
+}
+__device__ inline double rhs_ram(const halda_fleets &F, int64_t g, int set, double bcio) {
+    return rhs_ram(load_fields(F, g), set, bcio);
+}
+__device__ inline double rhs_cuda(const halda_fleets &F, int64_t g) { return rhs_cuda(load_fields(F, g)); }
+__device__ inline double rhs_metal(const halda_model &Mo, const halda_fleets &F, int64_t g) {
+    return rhs_metal(Mo, load_fields(F, g));
+}
+
+// Objective constants of one fleet (lane-parallel loads, the reference's sequential sums over
+// readlane): sum t_comm and sum xi in device order, kappa (dense_common.py:211-230) with its
+// M1 part before its M3 part (:226). Uniform on every lane.
+__device__ inline void fleet_offsets(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
+                                     double &tsum, double &xsum, double &kappa) {
+    tsum = 0.0;
+    xsum = 0.0;
+    double tail1 = 0.0;
+    int hi = -1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const double tc = F.t_comm[g];
+        const double xv = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const uint64_t heads = __ballot(i0 + lane < M && (F.flags[g] & HALDA_DEV_HEAD));
+        if (hi < 0 && heads) hi = i0 + __builtin_ctzll(heads);
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q) {
+            tsum += bcast(tc, q);
+            xsum += bcast(xv, q);
+            const int cq = bcast(cls, q);
+            if (cq == 1) tail1 += bcast(tl, q);
+        }
+    }
+    double tail = tail1;
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = min(i0 + lane, M - 1);
+        const int64_t g = d0 + i;
+        const int cls = F.os_class[g];
+        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const int n = min(64, M - i0);
+        for (int q = 0; q < n; ++q)
+            if (bcast(cls, q) == 3) tail += bcast(tl, q);
+    }
+    const int64_t h = d0 + (hi < 0 ? 0 : hi);
+    double total = f_over_s(Mo.has_f_out && (F.flags[h] & HALDA_DEV_CPU_RATE), Mo.f_out_b1, F.scpu_b1[h]);
+    total += (Mo.b_in / Mo.V + Mo.b_out) / F.T_cpu[h];
+    total += Mo.b_in / (Mo.V * F.s_disk[h]);
+    total += Mo.b_out / F.s_disk[h];
+    kappa = total + tail;
+}
+
+struct LowerOut {
+    halda_batch b;         // arrays written (device pointers, const-cast by the kernel)
+    int32_t *n_cols, *n_rows, *row_ptr, *col_idx;
+    int64_t *csr_off, *col_off, *row_off;
+    double *val, *c, *col_lb, *col_ub, *row_lb, *row_ub, *offs;  // offs[f]: t_comm sum, xi sum, kappa
+    uint8_t *integrality;
+};
+
+__global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_fleets F, const int32_t *ks, int n_k,
+                                                         LowerDims D, LowerOut O) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x;
+    if (f >= F.n_fleets) return;
+    const int64_t d0 = F.dev_off[f];
+    const int M = int(F.dev_off[f + 1] - d0);
+    const int64_t nnz0 = int64_t(f) * D.nnz;       // this fleet's CSR entries
+    const int64_t rp0 = int64_t(f) * (D.rows + 1);  // this fleet's row_ptr segment
+    const double bp = Mo.b_prime;
+    const int iC = 7 * M;
+    int rows = 0;
+    int64_t nnz = 0;
+    // per-block row emission: lane i emits up to 2 rows for device i (chunks of 64). Two passes of the
+    // row function: count the nonzeros, scan, then write the entries straight to the CSR (no private
+    // arrays: dynamically indexed ones would live in scratch).
+    auto emit = [&](auto &&row_fn) {
+        for (int i0 = 0; i0 < M; i0 += 64) {
+            const int i = i0 + lane;
+            const bool act = i < M;
+            int c0 = 0, c1 = 0;
+            double r0 = 0.0, r1 = 0.0;
+            const int nr = act ? row_fn(i, false, c0, c1, r0, r1, int64_t(0), int64_t(0)) : 0;
+            int rtot = 0, ntot = 0;
+            const int rbase = wave_excl_scan(nr, lane, &rtot);
+            const int nbase = wave_excl_scan(c0 + c1, lane, &ntot);
+            if (nr > 0) {
+                const int64_t e0 = nnz0 + nnz + nbase, e1 = e0 + c0;
+                int w0 = 0, w1 = 0;
+                row_fn(i, true, w0, w1, r0, r1, e0, e1);
+                const int r = rows + rbase;
+                O.row_ptr[rp0 + r] = int32_t(e0);
+                if (nr > 1) O.row_ptr[rp0 + r + 1] = int32_t(e1);
+                for (int j = 0; j < n_k; ++j) {
+                    if (Mo.L / ks[j] < M) continue;  // bound-infeasible: the screen reads only the eq row
+                    const int64_t ro = (int64_t(f) * n_k + j) * D.rows;
+                    O.row_lb[ro + r] = -kInf;
+                    O.row_ub[ro + r] = r0;
+                    if (nr > 1) {
+                        O.row_lb[ro + r + 1] = -kInf;
+                        O.row_ub[ro + r + 1] = r1;
+                    }
+                }
+            }
+            rows += rtot;
+            nnz += ntot;
+        }
+    };
+    // one (col, val) of a row when val != 0 (scipy builds its CSC from the dense rows): counted, or
+    // written at e + n when wr
+    auto put = [&](bool wr, int64_t e, int &n, int col, double v) {
+        if (v != 0.0) {
+            if (wr) {
+                O.col_idx[e + n] = col;
+                O.val[e + n] = v;
+            }
+            ++n;
+        }
+    };
+    // ---- per-device coefficients (lower._device_arrays order); lane i's own device is computed once
+    DevCoef mine = {};
+    if (lane < M) mine = dev_coef(Mo, F, d0 + lane);
+    auto coeff = [&](int i, double &alpha, double &b, double &p_bp, double &p_b, double &p_v, double &cst,
+                     double &bcio, double &xi) {
+        const DevCoef c = i == lane ? mine : dev_coef(Mo, F, d0 + i);
+        alpha = c.alpha; b = c.b; p_bp = c.p_bp; p_b = c.p_b; p_v = c.p_v; cst = c.cst; bcio = c.bcio; xi = c.xi;
+    };
+    // 1. link rows n_i - w_i <= 0
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+        (void)c1; (void)r1; (void)e1;
+        put(wr, e0, c0, i, -1.0);
+        put(wr, e0, c0, M + i, 1.0);
+        r0 = 0.0;
+        return 1;
+    });
+    // 2-4. RAM / Metal capacity rows by set
+    for (int set = 1; set <= 3; ++set) {
+        emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+            (void)c1; (void)r1; (void)e1;
+            const int64_t g = d0 + i;
+            if (F.os_class[g] != set) return 0;
+            if (set == 2 && !(F.flags[g] & HALDA_DEV_METAL_AVAIL)) return 0;
+            double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+            coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+            put(wr, e0, c0, i, bp);
+            if (set == 3) put(wr, e0, c0, M + i, -bp);
+            put(wr, e0, c0, (1 + set) * M + i, -bp);
+            r0 = rhs_ram(F, g, set, bcio);
+            return 1;
+        });
+    }
+    // 5. VRAM rows: per device the CUDA row, then the Metal row
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        const bool cu = fl & HALDA_DEV_CUDA_OK, me = fl & HALDA_DEV_METAL_OK;
+        const double rc = rhs_cuda(F, g);
+        const double rm = rhs_metal(Mo, F, g);
+        if (cu) {
+            put(wr, e0, c0, M + i, bp);
+            put(wr, e0, c0, 5 * M + i, -bp);
+            r0 = rc;
+        }
+        if (me) {
+            int &cm = cu ? c1 : c0;
+            const int64_t em = cu ? e1 : e0;
+            put(wr, em, cm, M + i, bp);
+            put(wr, em, cm, 5 * M + i, -bp);
+            (cu ? r1 : r0) = rm;
+        }
+        return int(cu) + int(me);
+    });
+    // 6. cycle rows busy + z - C <= -const ; busy + F - z - C <= -const
+    emit([&](int i, bool wr, int &c0, int &c1, double &r0, double &r1, int64_t e0, int64_t e1) {
+        double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+        coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+        put(wr, e0, c0, i, alpha);
+        put(wr, e1, c1, i, alpha + p_bp);
+        put(wr, e0, c0, M + i, b);
+        put(wr, e1, c1, M + i, b);
+        put(wr, e0, c0, 2 * M + i, p_bp);
+        put(wr, e1, c1, 2 * M + i, p_bp);
+        put(wr, e0, c0, 3 * M + i, p_b);
+        put(wr, e1, c1, 3 * M + i, p_b);
+        put(wr, e0, c0, 4 * M + i, p_bp);
+        put(wr, e1, c1, 4 * M + i, p_bp);
+        put(wr, e0, c0, 5 * M + i, p_v);
+        put(wr, e1, c1, 5 * M + i, p_v);
+        put(wr, e0, c0, 6 * M + i, 1.0);
+        put(wr, e1, c1, 6 * M + i, -1.0);
+        put(wr, e0, c0, iC, -1.0);
+        put(wr, e1, c1, iC, -1.0);
+        r0 = r1 = -cst;
+        return 2;
+    });
+    // 7. equality row sum_i w_i = W (row bounds per k below)
+    {
+        const int r = rows;
+        O.row_ptr[rp0 + r] = int32_t(nnz0 + nnz);
+        for (int i = lane; i < M; i += 64) {
+            O.col_idx[nnz0 + nnz + i] = i;
+            O.val[nnz0 + nnz + i] = 1.0;
+        }
+        nnz += M;
+        rows += 1;
+        if (lane == 0) O.row_ptr[rp0 + rows] = int32_t(nnz0 + nnz);
+    }
+    // ---- per-instance vectors (lane = device) and headers
+    for (int i0 = 0; i0 < M; i0 += 64) {
+        const int i = i0 + lane;
+        if (i >= M) continue;
+        const int64_t g = d0 + i;
+        const uint8_t fl = F.flags[g];
+        const int cls = F.os_class[g];
+        double alpha, b, p_bp, p_b, p_v, cst, bcio, xi;
+        coeff(i, alpha, b, p_bp, p_b, p_v, cst, bcio, xi);
+        const double busy[6] = {alpha, b, p_bp, p_b, p_bp, p_v};
+        const double gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1.0 : 0.0;
+        const double scale[6] = {1.0, gpu, cls == 1 ? 1.0 : 0.0, cls == 2 ? 1.0 : 0.0, cls == 3 ? 1.0 : 0.0, gpu};
+        for (int j = 0; j < n_k; ++j) {
+            const double W = double(Mo.L / ks[j]);
+            const int64_t co = (int64_t(f) * n_k + j) * D.cols;
+            if (Mo.L / ks[j] < M) {
+                // W < M = sum lb(w): the screen settles it from the w bounds (and c[C], the eq row)
+                O.col_lb[co + i] = 1.0;
+                O.col_ub[co + i] = W;
+                continue;
+            }
+#pragma unroll
+            for (int blk = 0; blk < 6; ++blk) {
+                O.c[co + blk * M + i] = busy[blk];
+                O.col_lb[co + blk * M + i] = blk == 0 ? 1.0 : 0.0;
+                O.col_ub[co + blk * M + i] = scale[blk] * W;
+                O.integrality[co + blk * M + i] = 1;
+            }
+            O.c[co + 6 * M + i] = 0.0;
+            O.col_lb[co + 6 * M + i] = 0.0;
+            O.col_ub[co + 6 * M + i] = kInf;
+            O.integrality[co + 6 * M + i] = 0;
+        }
+    }
+    for (int j = lane; j < n_k; j += 64) {
+        const int64_t inst = int64_t(f) * n_k + j;
+        const int64_t co = inst * D.cols, ro = inst * D.rows;
+        const double W = double(Mo.L / ks[j]);
+        O.c[co + iC] = double(ks[j] - 1);
+        O.col_lb[co + iC] = 0.0;
+        O.col_ub[co + iC] = kInf;
+        O.integrality[co + iC] = 0;
+        O.row_lb[ro + rows - 1] = W;
+        O.row_ub[ro + rows - 1] = W;
+        O.n_cols[inst] = 7 * M + 1;
+        O.n_rows[inst] = rows;
+        O.csr_off[inst] = rp0;
+        O.col_off[inst] = co;
+        O.row_off[inst] = ro;
+    }
+    // ---- objective offsets: sum t_comm and sum xi in device order, kappa (dense_common.py:211-230)
+    double tsum, xsum, kappa;
+    fleet_offsets(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    if (lane == 0) {
+        O.offs[3 * f + 0] = tsum;
+        O.offs[3 * f + 1] = xsum;
+        O.offs[3 * f + 2] = kappa;
+    }
+}
+
+// ---------------------------------------------------------------- fused k-sweep
+// halda_sweep_kernel: the whole `halda_solve` k-sweep of a fleet (halda_p_solver.py:369-436) in
+// one wave, from the fleet's device-field table, without materialising the MILPs. For every
+// k-candidate the wave builds, per device, exactly the record that decoding the lowered CSR
+// yields (load_dev of decode_cap_row / decode_cycle_row output, with the same rejections),
+// straight from the coefficients the lowering kernel writes into the CSR (dev_coef / rhs_* are
+// shared, so the values are the same bits); then settles bound-infeasible k (L / k < M), solves
+// k = 1 by the register greedy of the k = 1 fast path and the rest (k > 1, fleets wider than
+// 64 devices, fast-path fallbacks) by the general kernel's tables + DP / threshold scan, and keeps
+// the best k by the reference's rule (ascending k, strict "<" on obj_value, :407) in registers.
+// obj_value = c.x + sum t_comm + sum xi + kappa is formed in a fixed order (per-device costs
+// summed by a wave reduction, + (k - 1) C, + the fleet constants).
+//
+// kTables = false: no LDS; a fleet that needs a table is flagged (fflag[f] = 1, hb_flag = launch)
+// and left to the next launch. kTables = true: tables in the LDS slice (kGlobal = false) or in a
+// per-wave global slice (kGlobal = true); want = 1 selects the flagged fleets only (gated on the
+// hand-back flag), want = 0 every fleet.
+
+// Device record of table entry g, compact: the five coefficients, the least-slack offsets of its
+// RAM / Metal row and of its VRAM rows, its class and GPU flag; W = L / k is set per k. dev()
+// expands it to exactly the Dev that decoding the lowered CSR gives (load_dev of decode_cap_row /
+// decode_cycle_row output), so the solve code is shared; bad = 1 where decode would reject.
+struct FieldRec {
+    double alpha, b, p_bp, p_b, cst;
+    int Kset, Kvram;  // kNoRow: the row is absent
+    int cls, gpu, W;
+    __device__ inline Dev dev() const {
+        Dev d;
+        d.cw = alpha; d.cn = b; d.cs0 = p_bp; d.cs1 = p_b; d.cs2 = p_bp; d.cs3 = cls == 2 ? p_b : p_bp;
+        // cycle rows: busy + z - C <= -cst, busy + F - z - C <= -cst (w entries alpha, alpha + b'/s_disk)
+        d.r1w = alpha;
+        d.r2w = alpha + p_bp;
+        d.rhs1 = -cst;
+        d.rhs2 = -cst;
+        d.wlo = 1; d.whi = W; d.nlo = 0; d.nhi = gpu ? W : 0;
+        const bool hs = Kset != kNoRow, hv = Kvram != kNoRow;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const bool mine = cls == j + 1;
+            d.slo[j] = 0;
+            d.shi[j] = mine ? W : 0;
+            d.us[j] = mine && hs ? 1 : 0;
+            d.vs[j] = j == 2 && mine && hs ? -1 : 0;
+            d.Ks[j] = mine ? Kset : kNoRow;
+        }
+        d.slo[3] = 0; d.shi[3] = gpu ? W : 0; d.us[3] = 0; d.vs[3] = hv ? 1 : 0; d.Ks[3] = Kvram;
+        // the link row n - w <= 0 (scale 1: K = floor(0 + 1e-9) = 0)
+        d.uf[0] = -1; d.vf[0] = 1; d.Kf[0] = 0;
+        d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
+        return d;
+    }
+    __device__ inline FieldRec shfl(int src) const {  // per-lane source (all lanes active)
+        FieldRec o;
+        o.alpha = shfl_f64(alpha, src); o.b = shfl_f64(b, src); o.p_bp = shfl_f64(p_bp, src);
+        o.p_b = shfl_f64(p_b, src); o.cst = shfl_f64(cst, src);
+        o.Kset = __shfl(Kset, src); o.Kvram = __shfl(Kvram, src);
+        const int cg = __shfl(cls | (gpu << 4), src);
+        o.cls = cg & 15; o.gpu = cg >> 4;
+        o.W = W;
+        return o;
+    }
+    template <class SG>
+    __device__ inline auto bcast(const SG &sg, int src) const;  // the problem's device src, on every lane
+    __device__ inline const FieldRec &core() const { return *this; }
+};
+
+// A record broadcast to the whole problem (every lane holds device src's record): its split takes
+// the branches on the record's shape instead of selects (they are uniform here), skipping the
+// candidates the device does not have; the same candidates, order and tie rule as on a FieldRec.
+struct UFieldRec : FieldRec {
+    __device__ inline const UFieldRec &core() const { return *this; }
+};
+
+template <class SG>
+__device__ inline auto FieldRec::bcast(const SG &sg, int src) const {
+    UFieldRec o;
+    o.alpha = sg.bcast(alpha, src); o.b = sg.bcast(b, src); o.p_bp = sg.bcast(p_bp, src);
+    o.p_b = sg.bcast(p_b, src); o.cst = sg.bcast(cst, src);
+    o.Kset = sg.bcast(Kset, src); o.Kvram = sg.bcast(Kvram, src);
+    const int cg = sg.bcast(cls | (gpu << 4), src);
+    o.cls = cg & 15; o.gpu = cg >> 4;
+    o.W = W;
+    return o;
+}
+
+// The solve primitives on a FieldRec, specialised. The Dev that dev() expands a record to has two
+// live slacks: its class slack s_c >= w + Kset (class 3: w - n + Kset; s_c <= W) and the VRAM slack
+// t >= n + Kvram (t <= nhi), both priced pv = (class 2 ? p_b : p_bp), with 0 <= n <= min(w, nhi),
+// nhi = W on a GPU device, else 0; every other slack is pinned to 0 by its bounds. So split_full /
+// split_step / dev_cycle below visit the same candidates with the same tie rule as on dev() and give
+// the same bits: a pinned slack adds p * 0 = +0, which leaves any sum of terms >= +0 unchanged, and
+// where that term is NaN there (an infinite price of another class: inf * 0) the cost is NaN here.
+__device__ inline double rec_pv(const FieldRec &r) { return r.cls == 2 ? r.p_b : r.p_bp; }
+__device__ inline bool rec_own(const FieldRec &r) { return unsigned(r.cls - 1) < 3u; }
+__device__ inline bool rec_nanx(const FieldRec &r) { return r.p_bp == kInf || (r.p_b == kInf && r.cls != 2); }
+__device__ inline int rec_wlo(const FieldRec &) { return 1; }
+__device__ inline int rec_whi(const FieldRec &r) { return r.W; }
+
+// Feasible n-interval for w layers (n_interval on dev()); false when no n is feasible (also when
+// the class 1 / 2 slack, which does not depend on n, exceeds its bound).
+__device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) {
+    const bool hs = r.Kset != kNoRow;
+    const int nhi = r.gpu ? r.W : 0;
+    nL = r.cls == 3 && hs ? max(0, w + r.Kset - r.W) : 0;
+    nU = min(nhi, w);
+    nU = r.Kvram != kNoRow ? min(nU, nhi - r.Kvram) : nU;
+    const bool setok = !(hs && (r.cls == 1 || r.cls == 2)) || max(0, w + r.Kset) <= r.W;
+    return nL <= nU && setok;
+}
+
+// One candidate n of a split, branch-free (selects, non-short-circuit tests): dev_cost on dev() for
+// (w, n) and its least slacks (sc = the class slack, t = VRAM), in dev_cost's term order (aw = alpha
+// w, pv = rec_pv, own = rec_own), and the tie rule "smaller cost, then smaller n". The record's NaN
+// flag (rec_nanx) is applied by the caller: it fails the whole split, as a NaN cost at every
+// candidate does.
+__device__ inline void rec_try(const FieldRec &r, double aw, double pv, bool own, int w, int nn, int nL, int nU,
+                               double &best, int &bn) {
+    nn = min(max(nn, nL), nU);
+    const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
+    double g = aw;
+    g = g + r.b * double(nn);
+    const double gs = g + pv * double(sc);
+    g = own ? gs : g;
+    g = g + pv * double(t);
+    const bool better = (g < best) | ((g == best) & (nn < bn));
+    best = better ? g : best;
+    bn = better ? nn : bn;
+}
+
+__device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
+    const int sc = max(0, w - (r.cls == 3 ? n : 0) + r.Kset);
+    s[0] = r.cls == 1 ? sc : 0;
+    s[1] = r.cls == 2 ? sc : 0;
+    s[2] = r.cls == 3 ? sc : 0;
+    s[3] = max(0, n + r.Kvram);
+}
+
+// split_full on dev(): candidates nL, nU, the class-slack kink (class 3) and the VRAM kink, in that
+// order. Every candidate is evaluated on every lane (no divergent branches); an absent kink re-tries
+// nL, which never changes (best, bn): after nL's own try either bn = nL or best < cost(nL), and no
+// candidate lies below nL.
+template <bool kUniform>
+__device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    int nL, nU;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    const bool hc = r.cls == 3 && r.Kset != kNoRow, hv = r.Kvram != kNoRow;
+    if (!kUniform || hc) rec_try(r, aw, pv, own, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
+    if (!kUniform || hv) rec_try(r, aw, pv, own, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
+}
+__device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    return split_full_impl<false>(r, w, g, n, s);
+}
+// split_full at w = 1 (the record's lower bound): 0 <= nL <= n <= nU <= w = 1, so every kink clamps
+// to nL or nU and re-trying either is a no-op (after nU's try best <= cost(nU), and on a tie bn <= nU):
+// the two end tries give split_full's result.
+__device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    if (w != 1) return split_full(r, w, g, n, s);
+    int nL, nU;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
+}
+__device__ inline bool split_full(const UFieldRec &r, int w, double &g, int &n, int s[4]) {
+    return split_full_impl<true>(r, w, g, n, s);
+}
+
+__device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &g, int &n, int s[4]) {
+    int nL, nU;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, aw, pv, own, w, n_prev, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, n_prev + 1, nL, nU, best, bn);
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
+}
+
+// dev_cycle on dev(): rows (alpha, alpha + p_bp) w + b n + slack terms <= -cst.
+__device__ inline void dev_cycle(const FieldRec &r, int w, int n, const int s[4], double &P, double &Q) {
+    const double pv = rec_pv(r);
+    const int sc = r.cls == 1 ? s[0] : r.cls == 2 ? s[1] : s[2];
+    const double t0 = r.b * double(n), tc = pv * double(sc), tv = pv * double(s[3]);
+    double a1 = r.alpha * double(w), a2 = (r.alpha + r.p_bp) * double(w);
+    a1 = a1 + t0; a2 = a2 + t0;
+    const bool own = rec_own(r);
+    const double o1 = a1 + tc, o2 = a2 + tc;
+    a1 = own ? o1 : a1;
+    a2 = own ? o2 : a2;
+    a1 = a1 + tv; a2 = a2 + tv;
+    const bool nanx = rec_nanx(r);
+    a1 = nanx ? __builtin_nan("") : a1;
+    a2 = nanx ? __builtin_nan("") : a2;
+    P = a1 - (-r.cst);
+    Q = a2 - (-r.cst);
+}
+
+__device__ inline double least_cycle(const FieldRec &r, int w, int n, const int s[4]) {
+    double P, Q;
+    dev_cycle(r, w, n, s, P, Q);
+    return Q >= P ? 0.5 * (P + Q) : P;
+}
+
+__device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, int &bad) {
+    FieldRec r;
+    const DevCoef c = dev_coef(Mo, F);
+    const double bp = Mo.b_prime;
+    const int fl = F.flags;
+    r.alpha = c.alpha; r.b = c.b; r.p_bp = c.p_bp; r.p_b = c.p_b; r.cst = c.cst;
+    r.cls = F.cls;
+    r.gpu = (fl & (HALDA_DEV_CUDA_OK | HALDA_DEV_METAL_OK)) ? 1 : 0;
+    r.W = 0;
+    r.Kset = r.Kvram = kNoRow;
+    bad = !(fabs(c.cst) < 1e300);  // cycle-row rhs
+    bad |= !(c.p_bp >= 0.0) || !(c.p_b >= 0.0) || !(r.cls == 2 ? c.p_b >= 0.0 : c.p_bp >= 0.0);  // slack prices
+    // capacity rows b' u w + b' v n - b' s <= rhs -> s >= u w + v n + ceil(-rhs / b' - eps)
+    auto K = [&](double rhs, int &dst) {
+        if (!(bp > 0.0) || !(fabs(rhs) < 1e300)) {
+            bad = 1;
+            return;
+        }
+        const double kk = ceil(-rhs / bp - kSlackEps);
+        if (!(fabs(kk) < 1e8)) {
+            bad = 1;
+            return;
+        }
+        dst = max(dst, int(kk));
+    };
+    if (r.cls == 1 || r.cls == 3 || (fl & HALDA_DEV_METAL_AVAIL)) K(rhs_ram(F, r.cls, c.bcio), r.Kset);
+    // VRAM rows: CUDA or Metal (one division for either; both rows only on a device with both)
+    const bool cu = fl & HALDA_DEV_CUDA_OK, mt = fl & HALDA_DEV_METAL_OK;
+    if (cu && mt) {
+        K(rhs_cuda(F), r.Kvram);
+        K(rhs_metal(Mo, F), r.Kvram);
+    } else if (cu || mt) {
+        K(cu ? rhs_cuda(F) : rhs_metal(Mo, F), r.Kvram);
+    }
+    return r;
+}
+
+// Device records of a fleet straight from its table (the sweep's table path).
+// Device records of a fleet for the sweep's table path: for M <= 64 lane i already holds device
+// i's record (me), which other lanes fetch by shuffle; wider fleets rebuild it from the table.
+// load() runs on every lane (uniform control flow: the shuffles read every lane's registers).
+struct FieldSrc {
+    using Rec = FieldRec;
+    const halda_model *Mo;
+    const halda_fleets *F;
+    const FieldRec *me;  // lane's own record (M <= lanes per problem), or nullptr
+    int64_t d0;
+    int W;
+    int base;            // first lane of the problem's lane group
+    __device__ inline void load(FieldRec &r, const WaveCtx &, int i) const {
+        if (me) {
+            r = me->shfl(base + i);
+        } else {
+            int bad = 0;
+            r = field_rec(*Mo, load_fields(*F, d0 + i), bad);
+        }
+        r.W = W;
+    }
+};
+
+// Objective constants of a fleet for the sweep's own obj_value (a fixed tree order: wave
+// reductions): sum t_comm, sum xi, kappa with the head's terms (dense_common.py:211-230). For
+// M <= 64 lane i passes device i's fields (in registers) and the head's come by readlane.
+__device__ inline double tail_term(const DevFields &f) {
+    return f.cls != 2 ? double(f.ccpu - f.ram - f.swap) / f.sdisk : 0.0;
+}
+__device__ inline double xi_term(const DevFields &f) { return (f.r2v + f.v2r) * ((f.flags & HALDA_DEV_UMA) ? 0.0 : 1.0); }
+
+__device__ inline double kappa_head(const halda_model &Mo, int flags, double scpu, double Tc, double sdisk) {
+    double total = f_over_s(Mo.has_f_out && (flags & HALDA_DEV_CPU_RATE), Mo.f_out_b1, scpu);
+    total += (Mo.b_in / Mo.V + Mo.b_out) / Tc;
+    total += Mo.b_in / (Mo.V * sdisk);
+    total += Mo.b_out / sdisk;
+    return total;
+}
+
+template <class SG>
+__device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
+                                          double &xsum, double &kappa) {
+    const bool act = sg.sl < M;
+    // one wave sum for the three per-device constants of obj_value (t_comm, xi and kappa's tail term,
+    // added per device in that order): tsum carries all of it, xsum is 0 and kappa its head terms;
+    // obj_value's constants are summed in this fixed order (the host recomputes the reference's own
+    // order for halda_solve)
+    tsum = sg.sum_f64(act ? (mf.tcomm + xi_term(mf)) + tail_term(mf) : 0.0);
+    xsum = 0.0;
+    int hi = sg.lowest(act && (mf.flags & HALDA_DEV_HEAD));
+    if (hi >= SG::S) hi = 0;
+    // kappa_head's four quotients on lanes 0..3 of the problem (one division for the four), summed in
+    // its order
+    const int hf = sg.bcast(mf.flags, hi);
+    const double scpu = sg.bcast(mf.scpu, hi), Tc = sg.bcast(mf.Tc, hi), sdisk = sg.bcast(mf.sdisk, hi);
+    const double bv = Mo.b_in / Mo.V;
+    const int j = sg.sl & 3;
+    const double num = j == 0 ? Mo.f_out_b1 : j == 1 ? bv + Mo.b_out : j == 2 ? Mo.b_in : Mo.b_out;
+    const double den = j == 0 ? scpu : j == 1 ? Tc : j == 2 ? Mo.V * sdisk : sdisk;
+    const double q = num / den;
+    const double q0 = sg.bcast(q, 0), q1 = sg.bcast(q, 1), q2 = sg.bcast(q, 2), q3 = sg.bcast(q, 3);
+    double total = (Mo.has_f_out && (hf & HALDA_DEV_CPU_RATE)) ? (scpu > 0.0 ? 0.0 + q0 : 0.0) : 0.0;
+    total += q1;
+    total += q2;
+    total += q3;
+    kappa = total;
+}
+
+__device__ inline void fleet_offsets_tree(const halda_model &Mo, const halda_fleets &F, int64_t d0, int M, int lane,
+                                          double &tsum, double &xsum, double &kappa) {
+    double t = 0.0, x = 0.0, tail = 0.0;
+    int hi = 0x7fffffff;
+    for (int i = lane; i < M; i += 64) {
+        const DevFields f = load_fields(F, d0 + i);
+        t += f.tcomm;
+        x += xi_term(f);
+        tail += tail_term(f);
+        if (f.flags & HALDA_DEV_HEAD) hi = min(hi, i);
+    }
+    tsum = wave_sum_f64(t);
+    xsum = wave_sum_f64(x);
+    tail = wave_sum_f64(tail);
+    hi = wave_imin(hi);
+    const int64_t h = d0 + (hi == 0x7fffffff ? 0 : hi);
+    kappa = kappa_head(Mo, F.flags[h], F.scpu_b1[h], F.T_cpu[h], F.s_disk[h]) + tail;
+}
+
+// A uniform read of read-only memory through the scalar cache (s_load): the constant address space
+// tells the compiler the value cannot change under the kernel (a plain global read of a uniform
+// address is a vector load, a full memory round trip before the loads that depend on it).
+__device__ inline int64_t sload_i64(const int64_t *p) {
+    return *reinterpret_cast<const __attribute__((address_space(4))) int64_t *>(
+        reinterpret_cast<uintptr_t>(p));
+}
+
+// No instruction: the record's registers are redefined for the optimiser (stops loop-invariant
+// hoisting of values derived from it).
+__device__ inline void opaque_rec(FieldRec &r) {
+    asm volatile("" : "+v"(r.alpha), "+v"(r.b), "+v"(r.p_bp), "+v"(r.p_b), "+v"(r.cst), "+v"(r.Kset), "+v"(r.Kvram),
+                 "+v"(r.cls), "+v"(r.gpu));
+}
+
+// Kernel arguments. Everything a wave reads through the scalar cache comes first (six 64-B lines:
+// the model, the table pointers, the result pointers, the counts); the k list, which lanes read
+// with vector loads, last.
+// halda_fleet_result without x_off (ABI 2's compact layout travels at the end of SweepArgs): the
+// result pointers stay within the kernel arguments' first lines, read through the scalar cache.
+struct FleetOut {
+    int32_t *best_k;
+    double *obj_value;
+    int32_t *w, *n;
+    double *obj_by_k;
+    int32_t *status;
+    double *x, *c;
+    FleetOut() = default;
+    __host__ __device__ FleetOut(const halda_fleet_result &r)
+        : best_k(r.best_k), obj_value(r.obj_value), w(r.w), n(r.n), obj_by_k(r.obj_by_k), status(r.status), x(r.x),
+          c(r.c) {}
+};
+
+struct SweepArgs {
+    halda_model Mo;
+    halda_fleets F;
+    int n_k;
+    int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
+    FleetOut out;
+    int64_t xstride;
+    uint8_t *fflag;  // per fleet: 1 = needs the table launch
+    int *hb_flag;
+    int launch_id;
+    int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
+    int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
+    int xz;                        // 1: x / c of non-optimal instances written as zeros; 0: left as they are
+                                   // (the host zero-copy path zero-fills them on the host)
+    int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
+    unsigned char *gtab;           // kGlobal: per-wave slices
+    int64_t gstride;
+    const int64_t *x_off;          // halda_fleet_result.x_off (compact x / c layout) or nullptr
+    int32_t ks[64];  // the k list travels in the kernel arguments (no copy)
+    int32_t Ws[64];  // W = L / k per k (host integer division)
+};
+
+// x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
+// by the lane of each device when the caller asked for them.
+// Element offset of instance inst's x / c: the dense layout, or the caller's compact x_off (-1: not
+// written).
+__device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
+    return A.x_off ? A.x_off[inst] : inst * A.xstride;
+}
+
+__device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
+                              const FieldRec &r) {
+    if (!A.out.x && !A.out.c) return;
+    const int64_t at = xc_at(A, inst);
+    if (at < 0) return;
+    const Dev d = r.dev();
+    if (A.out.x) {
+        double *x = A.out.x + at;
+        x[i] = double(wl); x[M + i] = double(n);
+        x[2 * M + i] = double(s[0]); x[3 * M + i] = double(s[1]); x[4 * M + i] = double(s[2]);
+        x[5 * M + i] = double(s[3]); x[6 * M + i] = z;
+    }
+    if (A.out.c) {
+        double *c = A.out.c + at;
+        c[i] = d.cw; c[M + i] = d.cn; c[2 * M + i] = d.cs0; c[3 * M + i] = d.cs1; c[4 * M + i] = d.cs2;
+        c[5 * M + i] = d.cs3; c[6 * M + i] = 0.0;
+    }
+}
+
+#ifndef HALDA_SWEEP_TABLE_K1
+#define HALDA_SWEEP_TABLE_K1 1  // table launches also run the k = 1 register greedy (else k = 1 via tables)
+#endif
+
+__device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
+    // the scratch-free register launch (fflag == nullptr) never flags: sweep_fleets runs it alone only
+    // when nothing in the batch can need the table launch (no k > 1 with W >= M, R + 1 <= kDpLanes)
+    if (lane == 0 && A.fflag) {
+        A.fflag[f] = 1;
+        __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// SG = Wave: one fleet per wave; SG = Seg<16>: one fleet (M <= 16, n_k <= 16) per 16-lane segment,
+// tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
+// only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
+// the one-fleet-per-wave table launch, as the register-only launch does.
+template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false>
+__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg, const DevFields &pre = {},
+                            int64_t pre_base = 0) {
+    constexpr int S = SG::S;
+    constexpr bool kSeg = S < 64;
+    constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
+    const int lane = sg.sl;  // device index within the fleet
+    const halda_model &Mo = A.Mo;
+    const halda_fleets &F = A.F;
+    HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
+    // lane j: k_j and W_j = L / k_j (kernel arguments; their loads are issued with the fields')
+    const bool kl = lane < A.n_k;
+    const int kj = A.ks[kl ? lane : 0];
+    const int Wj = kl ? A.Ws[lane] : 0;
+    // the fleet's extent: with one fleet size for the batch, from dev_off[0] read through the scalar
+    // cache (the table is read-only to the kernel), so that the field loads are the wave's first
+    // vector round trip
+    // with one fleet size for the batch the first device is dev_off[0] + f uM; dev_off[0] (0 in the
+    // usual table) is read beside the field loads below, not in front of them
+    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM : F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
+    bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
+    if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
+    FieldRec me = {};
+    int bad = 0;
+    double tsum = 0.0, xsum = 0.0, kappa = 0.0;
+    if (regs) {
+        // every field of this lane's device in one round trip (lanes past M read device 0). With one
+        // fleet size the loads are issued at once from dev_off[0] = 0 (the usual table) while the
+        // scalar read of dev_off[0] is in flight, and reissued only where it is not 0: no dependent
+        // round trip in front of the field loads.
+        // pre: the caller loaded this lane's fields already (the pipelined kernel, one fleet size, its
+        // dev_off[0] = pre_base applied)
+        DevFields mf;
+        if constexpr (kPre) mf = pre;
+        else mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        if constexpr (kPre) {
+            d0 += pre_base;
+        } else if (A.uM > 0) {
+            // a vector read (returns in order behind the field loads: no wait of its own, unlike a
+            // scalar read, whose lgkmcnt wait would also hold the kernel-argument reads)
+            const int64_t base = __builtin_amdgcn_readfirstlane(int(F.dev_off[0])) |
+                                 (int64_t(__builtin_amdgcn_readfirstlane(int(uint64_t(F.dev_off[0]) >> 32))) << 32);
+            if (base != 0) {
+                d0 += base;
+                mf = load_fields(F, d0 + (lane < M ? lane : 0));
+            }
+        }
+        me = field_rec(Mo, mf, bad);
+        bad = lane < M ? bad : 0;
+        if (M > 0) fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
+    } else {
+        if (A.uM > 0) d0 += sload_i64(F.dev_off);
+        for (int i = lane; i < M; i += 64) {
+            int b1 = 0;
+            field_rec(Mo, load_fields(F, d0 + i), b1);
+            bad |= b1;
+        }
+        fleet_offsets_tree(Mo, F, d0, M, lane, tsum, xsum, kappa);
+    }
+    bad = sg.any(bad != 0) ? 1 : 0;
+    HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(9, __builtin_amdgcn_s_memrealtime());
+    double best = kInf;
+    int best_k = 0;
+    // the k's settled without a solve (the screen's verdicts: W >= 1e6 unsupported, M > W
+    // bound-infeasible, rows decode rejects) are written lane-parallel, and the loop below visits only
+    // the others, in ascending k
+    constexpr int kOpen = 1000;
+    int stj = kOpen;
+    if (!(Wj < 1000000)) stj = HALDA_STATUS_UNSUPPORTED;
+    else if (M > Wj) stj = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
+    else if (M > 0 && bad) stj = HALDA_STATUS_UNSUPPORTED;
+    if (kl && stj != kOpen) {
+        const int64_t inst = int64_t(f) * A.n_k + lane;
+        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
+        if (A.out.status) A.out.status[inst] = stj;
+    }
+    if (A.xz && (A.out.x || A.out.c)) {  // x / c of a settled instance are zero
+        uint64_t settled = sg.bits(kl && stj != kOpen);
+        const int N = 7 * M + 1;
+        while (settled) {
+            const int j = __builtin_ctzll(settled);
+            settled &= settled - 1;
+            const int64_t at = xc_at(A, int64_t(f) * A.n_k + j);
+            if (at >= 0)
+                for (int cc = lane; cc < N; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+    }
+    uint64_t todo = sg.bits(kl && stj == kOpen);
+    const int M_all = M;
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        // the record and M are opaque to the compiler at each k: nothing derived from them is hoisted
+        // out of this loop (hoisted per-lane masks and addresses held across the loop spill SGPRs; most
+        // fleets open one k)
+        opaque_rec(me);
+        int M = M_all;
+        if constexpr (!kSeg) asm volatile("" : "+s"(M));
+        const int k = sg.bcast(kj, j);
+        const int W = sg.bcast(Wj, j);
+        const int64_t inst = int64_t(f) * A.n_k + j;
+        const double kc = double(k - 1);
+        int st;
+        double obj = kInf;
+        bool improved = false;
+        if (M == 0) st = W > 0 ? HALDA_STATUS_INFEASIBLE : HALDA_STATUS_OPTIMAL;  // x = [C = 0]
+        else {
+            int rc = K1_FALLBACK, e = 0, rounds = 0, nE = 0;
+            double gE = 0.0;
+            bool haveE = true;  // gE / nE hold the split at w = 1 + e (k1_alloc), else split here
+            me.W = W;
+            if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
+            // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
+            // the solution for any k (the output adds (k - 1) max_i H_i)
+            if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M)) {
+                if constexpr (!kTables) {
+                    // the register launch solves its greedy fallbacks itself (exact DP, R + 1 <= kDpLanes)
+                    if (!A.k1dp) rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
+                    if (rc == K1_FALLBACK && W - M < kDpLanes) {
+                        rc = k1_dp(me, M, W - M, sg, e, w.dparg);
+                        haveE = false;
+                    }
+                } else {
+                    rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
+                }
+            }
+            if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
+            if (rc == K1_INFEASIBLE) {
+                st = HALDA_STATUS_INFEASIBLE;
+            } else if (rc == K1_OK) {
+                double g = 0.0, H = 0.0, z = 0.0;
+                int n = 0, sl[4] = {0, 0, 0, 0};
+                const int wl = 1 + e;
+                // the cycle times only matter through (k - 1) max H and the x output: at k = 1 without x
+                // the largest cycle time is not formed (kc * hmax is +0 either way: hmax is finite and
+                // >= 0 after a successful split)
+                const bool need_h = kc != 0.0 || A.out.x;
+                if (lane < M) {
+                    if (haveE) {
+                        g = gE;
+                        n = nE;
+                        rec_slacks(me, wl, n, sl);
+                    } else {
+                        split_full(me, wl, g, n, sl);
+                    }
+                    if (need_h) {
+                        double P, Q;
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        z = Q > P ? 0.5 * (Q - P) : 0.0;
+                        H = Q >= P ? 0.5 * (P + Q) : P;
+                    }
+                }
+                const double hmax = need_h ? fmax(0.0, sg.max_f64(lane < M ? H : 0.0)) : 0.0;
+                obj = sg.sum_f64(lane < M ? g : 0.0) + kc * hmax;
+                obj = obj + tsum;
+                obj = obj + xsum;
+                obj = obj + kappa;
+                st = HALDA_STATUS_OPTIMAL;
+                improved = obj < best;
+                if (lane < M) {
+                    put_xc(A, inst, M, lane, wl, n, sl, z, me);
+                    if (improved) {
+                        A.out.w[d0 + lane] = wl;
+                        A.out.n[d0 + lane] = n;
+                    }
+                }
+                if (lane == 0 && (A.out.x || A.out.c)) {
+                    const int64_t at = xc_at(A, inst);
+                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                }
+                HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
+            } else if constexpr (!kTables) {
+                // k > 1, a wide fleet or a fast-path fallback: the table launch redoes this fleet
+                flag_fleet(A, f, lane);
+                return;
+            } else {
+                if (kSeg && (kc == 0.0 || M < 2)) {  // a k = 1 fast-path fallback / one device: the 64-lane kernel
+                    flag_fleet(A, f, lane);
+                    return;
+                }
+                Inst I = {};
+                I.inst = int(inst);
+                HALDA_TSTAMP(0);
+                I.M = M;
+                I.W = W;
+                I.Wd = double(W);
+                I.kc = kc;
+                I.iC = 7 * M;
+                I.R1 = W - M + 1;
+                I.RS = odd_stride(I.R1);
+                const FieldSrc src{&A.Mo, &A.F, regs ? &me : nullptr, d0, W, sg.base};
+                int64_t nodes = 0;
+                const bool too_large =
+                    M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab);
+                if (kSeg && too_large) {
+                    flag_fleet(A, f, lane);
+                    return;
+                }
+                int feas = 1;
+                if (!too_large) {
+                    table_pass<S>(src, w, I, lane);
+                    wave_sync();
+                    HALDA_TSTAMP(6);
+                    if constexpr (kSeg) {
+                        feas = dp_pass_lanes(w, I, sg, nodes);
+                        if (feas < 0) {  // a leaf the incremental scan does not take
+                            flag_fleet(A, f, lane);
+                            return;
+                        }
+                    } else {
+                        feas = dp_pass(w, I, lane, nodes) ? 1 : 0;
+                    }
+                }
+                if (too_large) {
+                    st = HALDA_STATUS_TOO_LARGE;  // beyond the launch's slice (the host sizes it from the fleets)
+                } else if (!feas) {
+                    st = HALDA_STATUS_INFEASIBLE;
+                } else {
+                    HALDA_TSTAMP(7);
+                    // solution: per device (w, n, least slacks, z), sum of costs, largest cycle time
+                    double gs = 0.0, hmax = 0.0;
+                    for (int i0 = 0; i0 < M; i0 += S) {
+                        const int i = i0 + lane;
+                        FieldRec d;
+                        src.load(d, w, min(i, M - 1));
+                        if (i < M) {
+                            const int wl = 1 + w.st0[i];
+                            double g = 0.0, P, Q;
+                            int n = 0, sl[4] = {0, 0, 0, 0};
+                            split_full(d, wl, g, n, sl);
+                            dev_cycle(d, wl, n, sl, P, Q);
+                            gs += g;
+                            hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
+                            put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
+                        }
+                    }
+                    hmax = sg.max_f64(hmax);
+                    obj = sg.sum_f64(gs) + kc * hmax;
+                    obj = obj + tsum;
+                    obj = obj + xsum;
+                    obj = obj + kappa;
+                    st = HALDA_STATUS_OPTIMAL;
+                    improved = obj < best;
+                    if (improved)
+                        for (int i0 = 0; i0 < M; i0 += S) {
+                            const int i = i0 + lane;
+                            FieldRec d;
+                            src.load(d, w, min(i, M - 1));
+                            if (i < M) {
+                                const int wl = 1 + w.st0[i];
+                                double g;
+                                int n = 0, sl[4];
+                                split_full(d, wl, g, n, sl);
+                                A.out.w[d0 + i] = wl;
+                                A.out.n[d0 + i] = n;
+                            }
+                        }
+                    if (lane == 0 && (A.out.x || A.out.c)) {
+                        const int64_t at = xc_at(A, inst);
+                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                    }
+                    HALDA_TSTAMP(8);
+                }
+                wave_sync();  // tables / st0 are rewritten by the next k
+            }
+        }
+        if (st == HALDA_STATUS_OPTIMAL && M == 0) {
+            obj = 0.0;  // c.x = 0; no devices: the offsets are empty sums and kappa is undefined
+            improved = obj < best;
+            if (lane == 0 && (A.out.x || A.out.c)) {
+                const int64_t at = xc_at(A, inst);
+                if (at >= 0 && A.out.x) A.out.x[at] = 0.0;
+                if (at >= 0 && A.out.c) A.out.c[at] = kc;
+            }
+        }
+        if (improved) {
+            best = obj;
+            best_k = k;
+        }
+        if (A.xz && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
+            const int N = 7 * M + 1;
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = lane; cc < N; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+        if (lane == 0) {
+            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.out.status) A.out.status[inst] = st;
+        }
+    }
+    HALDA_SSTAMP(5, __builtin_amdgcn_s_memtime());
+    if (lane == 0) {
+        A.out.best_k[f] = best_k;
+        A.out.obj_value[f] = best;
+        if (kFirst && A.fflag) A.fflag[f] = 0;
+    }
+    if (best_k == 0)
+        for (int i = lane; i < M; i += S) {
+            A.out.w[d0 + i] = 0;
+            A.out.n[d0 + i] = 0;
+        }
+    HALDA_SSTAMP(6, __builtin_amdgcn_s_memtime());
+    HALDA_SSTAMP(8, __builtin_amdgcn_s_memrealtime());
+}
+
+template <bool kTables, bool kGlobal>
+__device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base) {
+    const int lane = threadIdx.x;
+    if (A.want == 1 && __hip_atomic_load(A.hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.launch_id)
+        return;
+    WaveCtx w = {};
+    if constexpr (kTables) {
+        const Slice sl = make_slice(A.mmax, A.r1max, A.tab, A.tab_kc);
+        unsigned char *base = slice_base;
+        w.rows = reinterpret_cast<int2 *>(base + sl.rows);
+        w.cyc = reinterpret_cast<double *>(base + sl.cyc);
+        w.cost = reinterpret_cast<double *>(base + sl.cost);
+        w.cnt = reinterpret_cast<int *>(base + sl.cnt);
+        w.st0 = reinterpret_cast<int *>(base + sl.st0);
+        w.st1 = reinterpret_cast<int *>(base + sl.st1);
+        w.rng = reinterpret_cast<int2 *>(base + sl.rng);
+        w.inc = reinterpret_cast<double *>(base + sl.inc);
+        w.G = reinterpret_cast<double *>(base + sl.G);
+        w.H = reinterpret_cast<double *>(base + sl.H);
+        w.work = reinterpret_cast<double *>(base + sl.work);
+        w.split = reinterpret_cast<uint16_t *>(base + sl.split);
+    }
+    const int S = gridDim.x;
+    const int nf = A.F.n_fleets;
+    for (int64_t b = blockIdx.x; b < nf; b += int64_t(64) * S) {
+        const int64_t mine = b + int64_t(lane) * S;
+        uint64_t todo = __ballot(mine < nf && (A.want == 0 || A.fflag[mine] == 1));
+        while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            sweep_fleet<kTables, kGlobal>(A, int(b + int64_t(bit) * S), w, Wave(lane));
+        }
+    }
+}
+
+#ifndef HALDA_SWEEP_WAVES_PER_SIMD
+#define HALDA_SWEEP_WAVES_PER_SIMD 4  // occupancy target of the register-only sweep (as the k = 1 kernel)
+#endif
+#ifndef HALDA_SWEEP_WPB
+#define HALDA_SWEEP_WPB 4
+#endif
+constexpr int kSweepWavesPerBlock = HALDA_SWEEP_WPB;  // fleets per workgroup of the register-only sweep
+
+// The register-only sweep: exactly one fleet per wave, kSweepWavesPerBlock waves per workgroup (a
+// quarter of the workgroups to dispatch); no loop, so no kernel argument stays live past its use.
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_kernel(SweepArgs A) {
+    // wave-uniform by construction; readfirstlane lets the compiler know (scalar fleet addressing)
+    const int f = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    {
+        // the kernel arguments the first branches read, fetched together with one value of every other
+        // 64-B line of SweepArgs the wave reads through the scalar cache (the model, the table and
+        // result pointers): one round trip instead of one per branch and line (each lgkmcnt wait would
+        // otherwise hold the next read back)
+        const int nf = A.F.n_fleets, nk = A.n_k, um = A.uM;
+        const int64_t *doff = A.F.dev_off;
+        const double bp = A.Mo.b_prime;
+        const double *tc = A.F.T_cpu;
+        const int32_t *ow = A.out.w;
+        asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
+    }
+    if (f >= A.F.n_fleets) return;
+    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
+    WaveCtx w = {};
+    w.dparg = dparg[threadIdx.x >> 6];
+    sweep_fleet<false, false>(A, f, w, Wave(int(threadIdx.x & 63)));
+}
+
+// The register-only sweep, pipelined: a grid of nw waves (fewer than the fleets), wave w takes fleets
+// w, w + nw, w + 2 nw, ... and issues the field loads of its next fleet before it solves the current
+// one, so the next fleet's memory round trip hides behind this fleet's compute and the dispatcher
+// launches nw waves instead of one per fleet. One fleet size for the batch (uM <= 64), else the
+// one-fleet-per-wave kernel runs. The per-fleet work is sweep_fleet's, bit for bit.
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_pipe_kernel(
+    SweepArgs A, int nw) {
+    const int wv = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    {
+        const int nf = A.F.n_fleets, nk = A.n_k, um = A.uM;
+        const int64_t *doff = A.F.dev_off;
+        const double bp = A.Mo.b_prime;
+        const double *tc = A.F.T_cpu;
+        const int32_t *ow = A.out.w;
+        asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
+    }
+    const int nf = A.F.n_fleets;
+    if (wv >= nf) return;
+    const int lane = threadIdx.x & 63;
+    const int M = A.uM;
+    const int li = lane < M ? lane : 0;
+    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
+    WaveCtx w = {};
+    w.dparg = dparg[threadIdx.x >> 6];
+    // the first fleet's fields from dev_off[0] = 0 (the usual table), reloaded where it is not 0
+    DevFields nxt = load_fields(A.F, int64_t(wv) * M + li);
+    const int64_t base = __builtin_amdgcn_readfirstlane(int(A.F.dev_off[0])) |
+                         (int64_t(__builtin_amdgcn_readfirstlane(int(uint64_t(A.F.dev_off[0]) >> 32))) << 32);
+    if (base != 0) nxt = load_fields(A.F, base + int64_t(wv) * M + li);
+    for (int f = wv; f < nf; f += nw) {
+        const DevFields cur = nxt;
+        const int fn = f + nw;
+        if (fn < nf) nxt = load_fields(A.F, base + int64_t(fn) * M + li);  // in flight during this fleet
+        sweep_fleet<false, false, Wave, true>(A, f, w, Wave(lane), cur, base);
+    }
+}
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    sweep_body<true, false>(A, smem);
+}
+
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_big_kernel(SweepArgs A) {
+    sweep_body<true, true>(A, A.gtab + int64_t(blockIdx.x) * A.gstride);
+}
+
+// halda_sweep_seg_kernel: fleets of at most kSegLanes devices (C2: 16) with at most kSegLanes
+// k-candidates, 64 / kSegLanes fleets per wave, one per lane segment, each with an LDS slice of only
+// what the lane-parallel path touches: G and H (k > 1 tables, row stride RS) and st0. Every wave
+// reduction of the one-fleet-per-wave path becomes a segment butterfly (same order of additions:
+// the wave butterfly's first two steps only add zeros for M <= 16), so the results are the same
+// bits; what the segment path does not take is flagged for the gated halda_sweep_tables_kernel.
+constexpr int kSegLanes = 16;
+
+__host__ __device__ inline int64_t seg_slice_bytes(int mmax, int tab_kc) {
+    return 2 * align16(int64_t(tab_kc) * 8) + align16(int64_t(mmax) * 4);
+}
+
+#ifndef HALDA_SEG_WAVES_PER_SIMD
+#define HALDA_SEG_WAVES_PER_SIMD 2
+#endif
+
+__global__ __launch_bounds__(64, HALDA_SEG_WAVES_PER_SIMD) void halda_sweep_seg_kernel(SweepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int kPer = 64 / kSegLanes;
+    const int lane = threadIdx.x;
+    const Seg<kSegLanes> sg(lane);
+    const int seg = lane / kSegLanes;
+    const int64_t tb = align16(int64_t(A.tab_kc) * 8);
+    unsigned char *base = smem + int64_t(seg) * seg_slice_bytes(A.mmax, A.tab_kc);
+    WaveCtx w = {};
+    w.G = reinterpret_cast<double *>(base);
+    w.H = reinterpret_cast<double *>(base + tb);
+    w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+    const int nf = A.F.n_fleets;
+    for (int64_t b = int64_t(blockIdx.x) * kPer; b < nf; b += int64_t(gridDim.x) * kPer) {
+        const int64_t f = b + seg;
+        if (f < nf) sweep_fleet<true, false, Seg<kSegLanes>>(A, int(f), w, sg);
+    }
+}
+
+// halda_sweep_kslot_kernel: the k-sweep of fleets of at most kSegLanes devices (C2) with the k's
+// spread over waves. A workgroup holds four fleets (one per 16-lane segment, as the segment kernel)
+// and one wave per open k-slot (the k's some fleet of the batch can take: L / k >= min_devices,
+// L / k < 1e6, ascending); wave q solves k-slot q of its four fleets -- the k = 1 register greedy,
+// the forced W = M split, or the k > 1 tables + threshold scan in its own LDS slice -- and leaves its
+// objective, status and (w, n) in the workgroup's pick area. After one barrier, wave 0 picks each
+// fleet's best k by the reference's rule (ascending k, strict "<" on obj_value,
+// halda_p_solver.py:407) and writes best_k / obj_value / w / n; the k's no slot takes (settled for
+// every fleet: M > W or W >= 1e6) are written there too. Same per-(fleet, k) arithmetic as
+// sweep_fleet on Seg<16> (the same records, reductions and tie rules: the same bits), but the
+// segment kernel's one wave per four fleets becomes one wave per (four fleets, k): four to sixteen
+// times the waves to hide the reductions' and LDS round trips' latency. What the slot waves cannot
+// take (greedy fallbacks, tables beyond the slice, non-convex leaves) flags the fleet for the gated
+// table launch, which redoes it whole.
+constexpr int kMaxSlots = 16;
+constexpr int kSlotFlagged = 1000;  // SlotPick.st: the fleet goes to the table launch
+
+struct SlotPick {  // one (segment, k-slot) result in the workgroup's pick area
+    double obj;    // obj_value when OPTIMAL, else +inf
+    int st;        // HALDA_STATUS_* or kSlotFlagged
+    int pad;
+    int w[kSegLanes], n[kSegLanes];
+};
+
+struct SlotArgs {
+    int n_slot;
+    int pick_off;              // LDS byte offset of the pick area (SlotPick [4][n_slot])
+    int j[kMaxSlots];          // k index of slot q (ascending)
+    int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * (R + 1) + max_devices, 0: no tables
+    int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
+    int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
+};
+
+// One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
+// its w / n candidate).
+__device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tabcap, const WaveCtx &w,
+                            const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec) {
+    using SG = Seg<kSegLanes>;
+    constexpr int S = SG::S;
+    const int lane = sg.sl;
+    const halda_model &Mo = A.Mo;
+    const halda_fleets &F = A.F;
+    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
+    const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+    int bad = 0;
+    FieldRec me = field_rec(Mo, mf, bad);
+    bad = lane < M ? bad : 0;
+    double tsum, xsum, kappa;
+    fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
+    const bool anybad = sg.any(bad != 0);
+#ifdef HALDA_STAMPS
+    *t_rec = __builtin_amdgcn_s_memtime();
+#else
+    (void)t_rec;
+#endif
+    const int k = A.ks[j], W = A.Ws[j];
+    const int64_t inst = int64_t(f) * A.n_k + j;
+    const double kc = double(k - 1);
+    int st;
+    double obj = kInf;
+    int wl = 0, nl = 0;  // this lane's (w, n) in the solution
+    if (!(W < 1000000)) st = HALDA_STATUS_UNSUPPORTED;
+    else if (M > W) st = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
+    else if (anybad) st = HALDA_STATUS_UNSUPPORTED;
+    else {
+        me.W = W;
+        if (k == 1 || W == M) {
+            // the register greedy; W = M (R = 0): every w_i = 1 is forced
+            int e = 0, rounds = 0, nE = 0;
+            double gE = 0.0;
+            const int rc = k1_alloc(me, M, W - M, sg, e, rounds, gE, nE);
+            if (rc == K1_INFEASIBLE) {
+                st = HALDA_STATUS_INFEASIBLE;
+            } else if (rc == K1_OK) {
+                double g = 0.0, H = 0.0, z = 0.0;
+                int n = 0, sl[4] = {0, 0, 0, 0};
+                wl = 1 + e;
+                const bool need_h = kc != 0.0 || A.out.x;
+                if (lane < M) {
+                    g = gE;
+                    n = nE;
+                    rec_slacks(me, wl, n, sl);
+                    if (need_h) {
+                        double P, Q;
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        z = Q > P ? 0.5 * (Q - P) : 0.0;
+                        H = Q >= P ? 0.5 * (P + Q) : P;
+                    }
+                }
+                const double hmax = need_h ? fmax(0.0, sg.max_f64(lane < M ? H : 0.0)) : 0.0;
+                obj = sg.sum_f64(lane < M ? g : 0.0) + kc * hmax;
+                obj = obj + tsum;
+                obj = obj + xsum;
+                obj = obj + kappa;
+                st = HALDA_STATUS_OPTIMAL;
+                nl = n;
+                if (lane < M) put_xc(A, inst, M, lane, wl, n, sl, z, me);
+                if (lane == 0 && (A.out.x || A.out.c)) {
+                    const int64_t at = xc_at(A, inst);
+                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                }
+            } else {
+                st = kSlotFlagged;  // a greedy fallback: the 64-lane table launch
+            }
+        } else if (M < 2) {
+            st = kSlotFlagged;
+        } else {
+            Inst I = {};
+            I.inst = int(inst);
+            I.M = M;
+            I.W = W;
+            I.Wd = double(W);
+            I.kc = kc;
+            I.iC = 7 * M;
+            I.R1 = W - M + 1;
+            I.RS = odd_stride(I.R1);
+            if (M > A.mmax || I.R1 > r1cap || int64_t(M) * I.RS > tabcap) {
+                st = kSlotFlagged;  // beyond the slot's slice
+            } else {
+                const FieldSrc src{&A.Mo, &A.F, &me, d0, W, sg.base};
+                int64_t nodes = 0;
+                table_pass<S>(src, w, I, lane);
+                wave_sync();
+                const int feas = dp_pass_lanes(w, I, sg, nodes);
+                if (feas < 0) {
+                    st = kSlotFlagged;  // a leaf the incremental scan does not take
+                } else if (!feas) {
+                    st = HALDA_STATUS_INFEASIBLE;
+                } else {
+                    double g = 0.0, P = 0.0, Q = 0.0, hmax = 0.0;
+                    int n = 0, sl[4] = {0, 0, 0, 0};
+                    if (lane < M) {
+                        wl = 1 + w.st0[lane];
+                        split_full(me, wl, g, n, sl);
+                        dev_cycle(me, wl, n, sl, P, Q);
+                        hmax = Q >= P ? 0.5 * (P + Q) : P;
+                        put_xc(A, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
+                    }
+                    hmax = sg.max_f64(fmax(0.0, hmax));
+                    obj = sg.sum_f64(0.0 + g) + kc * hmax;  // the segment kernel's sum (0.0 + g per lane)
+                    obj = obj + tsum;
+                    obj = obj + xsum;
+                    obj = obj + kappa;
+                    st = HALDA_STATUS_OPTIMAL;
+                    nl = n;
+                    if (lane == 0 && (A.out.x || A.out.c)) {
+                        const int64_t at = xc_at(A, inst);
+                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                    }
+                }
+            }
+        }
+    }
+    if (st == kSlotFlagged) {
+        flag_fleet(A, f, lane);
+    } else {
+        if (lane == 0) {
+            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.out.status) A.out.status[inst] = st;
+        }
+        if (A.xz && st != HALDA_STATUS_OPTIMAL && (A.out.x || A.out.c)) {  // x / c of a non-optimal instance
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = lane; cc < 7 * M + 1; cc += S) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+    }
+    if (lane == 0) {
+        pk->obj = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+        pk->st = st;
+    }
+    if (lane < M) {
+        pk->w[lane] = wl;
+        pk->n[lane] = nl;
+    }
+}
+
+// The pick of one fleet (segment lanes): best k over the slots in ascending k with strict "<", the
+// settled k's of no slot, best_k / obj_value / w / n and the fleet's flag byte.
+__device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const SlotPick *pk, const Seg<kSegLanes> &sg) {
+    constexpr int S = kSegLanes;
+    const int lane = sg.sl;
+    const int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + A.F.dev_off[0] : A.F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(A.F.dev_off[f + 1] - d0);
+    bool flagged = false;
+    double best = kInf;
+    int bq = -1;
+    for (int q = 0; q < SA.n_slot; ++q) {
+        const int st = pk[q].st;
+        flagged = flagged || st == kSlotFlagged;
+        if (st == HALDA_STATUS_OPTIMAL && pk[q].obj < best) {
+            best = pk[q].obj;
+            bq = q;
+        }
+    }
+    if (flagged) return;  // the table launch redoes this fleet (fflag / hb_flag set by the slot wave)
+    // k's of no slot: settled for every fleet of the batch (W >= 1e6 unsupported, else M > W)
+    for (int jj = lane; jj < A.n_k; jj += S) {
+        bool slot = false;
+        for (int q = 0; q < SA.n_slot; ++q) slot = slot || SA.j[q] == jj;
+        if (slot) continue;
+        const int64_t inst = int64_t(f) * A.n_k + jj;
+        const int st = !(A.Ws[jj] < 1000000) ? HALDA_STATUS_UNSUPPORTED : HALDA_STATUS_INFEASIBLE;
+        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
+        if (A.out.status) A.out.status[inst] = st;
+        if (A.xz && (A.out.x || A.out.c)) {
+            const int64_t at = xc_at(A, inst);
+            if (at >= 0)
+                for (int cc = 0; cc < 7 * M + 1; ++cc) {
+                    if (A.out.x) A.out.x[at + cc] = 0.0;
+                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                }
+        }
+    }
+    if (lane == 0) {
+        A.out.best_k[f] = bq >= 0 ? A.ks[SA.j[bq]] : 0;
+        A.out.obj_value[f] = best;
+        A.fflag[f] = 0;
+    }
+    if (lane < M) {
+        A.out.w[d0 + lane] = bq >= 0 ? pk[bq].w[lane] : 0;
+        A.out.n[d0 + lane] = bq >= 0 ? pk[bq].n[lane] : 0;
+    }
+}
+
+__global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int kPer = 64 / kSegLanes;
+    const int lane = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // this wave's k-slot
+    const Seg<kSegLanes> sg(lane);
+    const int seg = lane / kSegLanes;
+    const int nf = A.F.n_fleets;
+    const int64_t f = int64_t(blockIdx.x) * kPer + seg;
+    SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
+    HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
+    HALDA_KSTAMPW(5, __builtin_amdgcn_s_memrealtime());
+    {
+        const int tab = SA.tab[q];
+        const int64_t tb = align16(int64_t(tab) * 8);
+        unsigned char *base = smem + SA.off[q] + int64_t(seg) * seg_slice_bytes(A.mmax, tab);
+        WaveCtx w = {};
+        w.G = reinterpret_cast<double *>(base);
+        w.H = reinterpret_cast<double *>(base + tb);
+        w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+        unsigned long long t_rec = 0;
+        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q, &t_rec);
+        HALDA_KSTAMPW(1, t_rec);
+    }
+    HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
+    __syncthreads();
+    HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
+    if (q == 0 && f < nf) kslot_pick(A, SA, int(f), pick + seg * SA.n_slot, sg);
+    HALDA_KSTAMPW(4, __builtin_amdgcn_s_memtime());
+}
+
+// halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +
+// sum xi + kappa (halda_p_solver.py:356-357), best k by ascending k with strict
+// "<" (halda_p_solver.py:407), w / n of the winner (int(round(x)), :350-351).
+__global__ __launch_bounds__(64) void halda_pick_kernel(halda_batch B, halda_result R, halda_fleets F, int n_k,
+                                                        const double *offs, halda_fleet_result out, int64_t xstride) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x;
+    if (f >= F.n_fleets) return;
+    int best_j = -1;
+    double best = kInf;
+    for (int j = 0; j < n_k; ++j) {
+        const int64_t inst = int64_t(f) * n_k + j;
+        const int st = R.status[inst];
+        double obj = kInf;
+        if (st == HALDA_STATUS_OPTIMAL) {
+            const int64_t co = B.col_off[inst];
+            const int N = B.n_cols[inst];
+            double part = 0.0;
+            for (int c = lane; c < N; c += 64) part += B.c[co + c] * R.x[co + c];
+            obj = wave_sum_f64(part);
+            obj = obj + offs[3 * f + 0];
+            obj = obj + offs[3 * f + 1];
+            obj = obj + offs[3 * f + 2];
+            if (obj < best) {
+                best = obj;
+                best_j = j;
+            }
+        }
+        if (lane == 0) {
+            if (out.obj_by_k) out.obj_by_k[inst] = obj;
+            if (out.status) out.status[inst] = st;
+        }
+        const int64_t at = out.x_off ? out.x_off[inst] : inst * xstride;
+        if ((out.x || out.c) && at >= 0) {
+            const int64_t co = B.col_off[inst];
+            const int N = B.n_cols[inst];
+            for (int cc = lane; cc < N; cc += 64) {
+                if (out.x) out.x[at + cc] = st == HALDA_STATUS_OPTIMAL ? R.x[co + cc] : 0.0;
+                if (out.c) out.c[at + cc] = st == HALDA_STATUS_OPTIMAL ? B.c[co + cc] : 0.0;
+            }
+        }
+    }
+    const int64_t d0 = F.dev_off[f];
+    const int M = int(F.dev_off[f + 1] - d0);
+    if (lane == 0) {
+        out.best_k[f] = best_j >= 0 ? int(B.c[B.col_off[int64_t(f) * n_k + best_j] + 7 * M]) + 1 : 0;
+        out.obj_value[f] = best;
+    }
+    for (int i = lane; i < M; i += 64) {
+        int w = 0, n = 0;
+        if (best_j >= 0) {
+            const int64_t co = B.col_off[int64_t(f) * n_k + best_j];
+            w = int(rint(R.x[co + i]));
+            n = int(rint(R.x[co + M + i]));
+        }
+        out.w[d0 + i] = w;
+        out.n[d0 + i] = n;
+    }
+}
