@@ -232,13 +232,18 @@ def run_cpu_baseline(budget_s: float, M: int):
 
 
 # ------------------------------------------------------------------ GPU legs
-def timed(step, steps, torch, dev, dist, world):
+HOST_ENQUEUE = {}  # per timed leg: host seconds to enqueue its K steps (before the final synchronize)
+
+
+def timed(step, steps, torch, dev, dist, world, tag=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if tag:
+        HOST_ENQUEUE[tag] = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -442,7 +447,7 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     turn = [0]
 
     def step2():
-        tabs[turn[0] % n].launch(ctx, srefs[turn[0] % 2])
+        tabs[turn[0] % n].launch(ctx, srefs[turn[0] % len(srefs)])
         turn[0] += 1
 
     def step1():
@@ -504,7 +509,7 @@ def main():
     ap.add_argument("--fleets", type=int, default=C3_FLEETS, help="fleets per GPU per step (weak scaling)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="headline: weak (fleets per GPU fixed) or strong (4096 fleets in total)")
-    ap.add_argument("--streams", type=int, choices=(1, 2), default=2,
+    ap.add_argument("--streams", type=int, choices=(1, 2, 3, 4), default=2,
                     help="streams the k-sweep steps alternate over (1: every launch serialised, e.g. for "
                          "per-dispatch profiling)")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
@@ -578,8 +583,8 @@ def main():
     sref = stream.cuda_stream
     # the k-sweep steps alternate between two streams: consecutive batches are independent (own
     # tables and results), so one batch's field loads overlap the previous batch's compute tail
-    stream2 = torch.cuda.Stream(dev)
-    srefs = [sref, stream2.cuda_stream] if args.streams == 2 else [sref, sref]
+    extra = [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
+    srefs = [sref] + [x.cuda_stream for x in extra]
 
     # ---- headline: the k-sweep from resident device-field tables (rotating copies > the MALL)
     tbytes = DeviceFleetTable(table, model, ks, 0.5, dev).nbytes()
@@ -588,7 +593,7 @@ def main():
     turn = [0, 0]  # per leg: which resident copy the next step reads
 
     def sweep_step():
-        sweeps[turn[0] % n_sw].launch(ctx, srefs[turn[0] % 2])
+        sweeps[turn[0] % n_sw].launch(ctx, srefs[turn[0] % len(srefs)])
         turn[0] += 1
 
     def sweep_step_one_stream():
@@ -623,7 +628,7 @@ def main():
         raise RuntimeError("a fleet without a feasible k in the sweep")
 
     ctx.set_timing(False)  # no per-launch instrumentation events inside the timed regions
-    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world)
+    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world, tag="headline")
     el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world)
     sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream)
     el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
@@ -636,7 +641,7 @@ def main():
         sturn = [0]
 
         def strong_step():
-            s_sweeps[sturn[0] % n_st].launch(ctx, srefs[sturn[0] % 2])
+            s_sweeps[sturn[0] % n_st].launch(ctx, srefs[sturn[0] % len(srefs)])
             sturn[0] += 1
 
         for _ in range(args.warmup):
@@ -696,6 +701,8 @@ def main():
             },
             "one_stream": {"what": "the same k-sweep steps all on one stream (each batch waits for the previous)",
                            "ms_per_step": el_sweep1 / args.steps * 1e3, "instances_per_s": total / el_sweep1},
+            "host_enqueue_ms_per_step": HOST_ENQUEUE["headline"] / args.steps * 1e3,
+            "streams": args.streams,
             "feasible_instances_per_s": value * n_opt / batch.n_inst,
             "fleets_per_s": n_fleets_total / el_sweep,
             "time_to_optimal_ms": tto,

@@ -366,6 +366,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     }
     A.n_k = n_k;
     A.out = FleetOut(out);
+    A.outs = (out.obj_by_k ? kOutObk : 0) | (out.status ? kOutSt : 0) | (out.x ? kOutX : 0) | (out.c ? kOutC : 0) |
+             (c->x_zero ? kOutXZ : 0);
     A.x_off = out.x_off;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
     A.fflag = scratch ? static_cast<uint8_t *>(c->fflag) + 256 : nullptr;
@@ -374,7 +376,6 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     A.mmax = mmax;
     A.uM = F.min_devices == F.max_devices ? F.max_devices : 0;
     A.k1dp = c->k1_force_dp ? 1 : 0;
-    A.xz = c->x_zero ? 1 : 0;
     A.r1max = int(r1max);
     A.tab = int(tab);
     A.tab_kc = int(tab_kc);

@@ -18,7 +18,7 @@ enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3, CLS_BIG = 4 };
 // Diagnostic build only (-DHALDA_STAMPS): per-instance s_memtime stamps at the
 // phase boundaries of the solve kernel, read back with halda_debug_stamps().
 #ifdef HALDA_STAMPS
-constexpr int kStampInst = 65536, kStamps = 10;
+constexpr int kStampInst = 65536, kStamps = 12;
 __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 #define HALDA_STAMP(k)                                                                                  \
     do {                                                                                                \

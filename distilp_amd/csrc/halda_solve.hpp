@@ -932,9 +932,19 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
         typename Src::Rec d;
         src.load(d, w, min(i, I.M - 1));
         if (i < I.M) {
-            int n = 0;
-            bool have = false;
-            for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
+            // 16-lane segments (the k-slot / segment sweeps, one device per lane): two independent
+            // chains per lane, e in [0, h) and [h, R1), advanced in the same iteration (the second
+            // starts with a full split search, as a stretch of the P-lane layout above: the same least
+            // minimisers, so the same G and H); their dependent split / cycle-time arithmetic
+            // interleaves instead of one chain of R1 entries. (The 64-lane kernels keep one chain: their
+            // register budget is spent elsewhere.)
+            const int h = S == 16 ? (I.R1 + 1) / 2 : I.R1;
+            int na = 0, nb = 0;
+            bool ha = false, hb = false;
+            for (int e = 0; e < h; ++e) {
+                table_entry(d, w, I, i, e, na, ha);
+                if (S == 16 && h + e < I.R1) table_entry(d, w, I, i, h + e, nb, hb);
+            }
         }
     }
 }
@@ -1072,7 +1082,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
 // lowest device, runs taken while they beat the runner-up), then the incremental threshold scan.
 // Returns 1 solved (st0 = allocation), 0 infeasible, -1 not applicable (the table DP below runs).
 template <class SG>
-__device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int64_t &nodes) {
+__device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int64_t &nodes,
+                             unsigned long long *stamp = nullptr) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const int lane = sg.sl;
     const bool act = lane < M;
@@ -1081,6 +1092,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     bool ok = true, mono = true;
     double prev = kInf, dprev = -kInf, hprev = -kInf;
     if (act)
+#pragma unroll 4
         for (int e = 0; e < R1; ++e) {
             const double g = G[e], h = H[e];
             if (g < kInf) {
@@ -1099,6 +1111,11 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
         }
     if (sg.any(act && (!ok || !mono))) return -1;
     if (sg.any(act && cnt == 0)) return 0;
+#ifdef HALDA_STAMPS
+    if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();  // leaf scan done
+#else
+    (void)stamp;
+#endif
     LeafInfo li;
     li.convex = true;
     li.mono = true;
@@ -1130,6 +1147,9 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     const double hmax = sg.max_f64(act ? fmax(0.0, H[e]) : 0.0);
     if (act) w.st0[lane] = e;
     nodes = 1;
+#ifdef HALDA_STAMPS
+    if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();  // phase-0 greedy done
+#endif
     kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li);
     wave_sync();
     return 1;

@@ -768,11 +768,16 @@ struct FleetOut {
           c(r.c) {}
 };
 
+// SweepArgs.outs: which optional outputs the call wants, in one word the waves read with the first
+// kernel-argument line (testing the pointers themselves costs a dependent scalar load each)
+constexpr int kOutObk = 1, kOutSt = 2, kOutX = 4, kOutC = 8, kOutXC = kOutX | kOutC, kOutXZ = 16;
+
 struct SweepArgs {
     halda_model Mo;
     halda_fleets F;
     int n_k;
     int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
+    int outs;                      // kOut* bits
     FleetOut out;
     int64_t xstride;
     uint8_t *fflag;  // per fleet: 1 = needs the table launch
@@ -780,8 +785,6 @@ struct SweepArgs {
     int launch_id;
     int want;                      // 0: every fleet, 1: flagged fleets (gated on hb_flag)
     int k1dp;                      // register sweep: 1 = every k = 1 / W = M instance by k1_dp (test path)
-    int xz;                        // 1: x / c of non-optimal instances written as zeros; 0: left as they are
-                                   // (the host zero-copy path zero-fills them on the host)
     int mmax, r1max, tab, tab_kc;  // table slice shape (kTables)
     unsigned char *gtab;           // kGlobal: per-wave slices
     int64_t gstride;
@@ -790,27 +793,27 @@ struct SweepArgs {
     int32_t Ws[64];  // W = L / k per k (host integer division)
 };
 
-// x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
-// by the lane of each device when the caller asked for them.
 // Element offset of instance inst's x / c: the dense layout, or the caller's compact x_off (-1: not
 // written).
 __device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
     return A.x_off ? A.x_off[inst] : inst * A.xstride;
 }
 
+// x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
+// by the lane of each device when the caller asked for them.
 __device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
                               const FieldRec &r) {
-    if (!A.out.x && !A.out.c) return;
+    if (!(A.outs & kOutXC)) return;
     const int64_t at = xc_at(A, inst);
     if (at < 0) return;
     const Dev d = r.dev();
-    if (A.out.x) {
+    if (A.outs & kOutX) {
         double *x = A.out.x + at;
         x[i] = double(wl); x[M + i] = double(n);
         x[2 * M + i] = double(s[0]); x[3 * M + i] = double(s[1]); x[4 * M + i] = double(s[2]);
         x[5 * M + i] = double(s[3]); x[6 * M + i] = z;
     }
-    if (A.out.c) {
+    if (A.outs & kOutC) {
         double *c = A.out.c + at;
         c[i] = d.cw; c[M + i] = d.cn; c[2 * M + i] = d.cs0; c[3 * M + i] = d.cs1; c[4 * M + i] = d.cs2;
         c[5 * M + i] = d.cs3; c[6 * M + i] = 0.0;
@@ -910,10 +913,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     else if (M > 0 && bad) stj = HALDA_STATUS_UNSUPPORTED;
     if (kl && stj != kOpen) {
         const int64_t inst = int64_t(f) * A.n_k + lane;
-        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
-        if (A.out.status) A.out.status[inst] = stj;
+        if (A.outs & kOutObk) A.out.obj_by_k[inst] = kInf;
+        if (A.outs & kOutSt) A.out.status[inst] = stj;
     }
-    if (A.xz && (A.out.x || A.out.c)) {  // x / c of a settled instance are zero
+    if ((A.outs & kOutXZ) && (A.outs & kOutXC)) {  // x / c of a settled instance are zero
         uint64_t settled = sg.bits(kl && stj != kOpen);
         const int N = 7 * M + 1;
         while (settled) {
@@ -922,8 +925,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             const int64_t at = xc_at(A, int64_t(f) * A.n_k + j);
             if (at >= 0)
                 for (int cc = lane; cc < N; cc += S) {
-                    if (A.out.x) A.out.x[at + cc] = 0.0;
-                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
                 }
         }
     }
@@ -976,7 +979,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 // the cycle times only matter through (k - 1) max H and the x output: at k = 1 without x
                 // the largest cycle time is not formed (kc * hmax is +0 either way: hmax is finite and
                 // >= 0 after a successful split)
-                const bool need_h = kc != 0.0 || A.out.x;
+                const bool need_h = kc != 0.0 || (A.outs & kOutX);
                 if (lane < M) {
                     if (haveE) {
                         g = gE;
@@ -1006,10 +1009,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                         A.out.n[d0 + lane] = n;
                     }
                 }
-                if (lane == 0 && (A.out.x || A.out.c)) {
+                if (lane == 0 && (A.outs & kOutXC)) {
                     const int64_t at = xc_at(A, inst);
-                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
-                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                    if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
                 }
                 HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
             } else if constexpr (!kTables) {
@@ -1098,10 +1101,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                                 A.out.n[d0 + i] = n;
                             }
                         }
-                    if (lane == 0 && (A.out.x || A.out.c)) {
+                    if (lane == 0 && (A.outs & kOutXC)) {
                         const int64_t at = xc_at(A, inst);
-                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
-                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                        if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
                     }
                     HALDA_TSTAMP(8);
                 }
@@ -1111,28 +1114,28 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         if (st == HALDA_STATUS_OPTIMAL && M == 0) {
             obj = 0.0;  // c.x = 0; no devices: the offsets are empty sums and kappa is undefined
             improved = obj < best;
-            if (lane == 0 && (A.out.x || A.out.c)) {
+            if (lane == 0 && (A.outs & kOutXC)) {
                 const int64_t at = xc_at(A, inst);
-                if (at >= 0 && A.out.x) A.out.x[at] = 0.0;
-                if (at >= 0 && A.out.c) A.out.c[at] = kc;
+                if (at >= 0 && (A.outs & kOutX)) A.out.x[at] = 0.0;
+                if (at >= 0 && (A.outs & kOutC)) A.out.c[at] = kc;
             }
         }
         if (improved) {
             best = obj;
             best_k = k;
         }
-        if (A.xz && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
+        if ((A.outs & kOutXZ) && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
             const int N = 7 * M + 1;
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = lane; cc < N; cc += S) {
-                    if (A.out.x) A.out.x[at + cc] = 0.0;
-                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
                 }
         }
         if (lane == 0) {
-            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
-            if (A.out.status) A.out.status[inst] = st;
+            if (A.outs & kOutObk) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.outs & kOutSt) A.out.status[inst] = st;
         }
     }
     HALDA_SSTAMP(5, __builtin_amdgcn_s_memtime());
@@ -1350,7 +1353,7 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
     fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
     const bool anybad = sg.any(bad != 0);
 #ifdef HALDA_STAMPS
-    *t_rec = __builtin_amdgcn_s_memtime();
+    t_rec[0] = __builtin_amdgcn_s_memtime();
 #else
     (void)t_rec;
 #endif
@@ -1376,7 +1379,7 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
                 double g = 0.0, H = 0.0, z = 0.0;
                 int n = 0, sl[4] = {0, 0, 0, 0};
                 wl = 1 + e;
-                const bool need_h = kc != 0.0 || A.out.x;
+                const bool need_h = kc != 0.0 || (A.outs & kOutX);
                 if (lane < M) {
                     g = gE;
                     n = nE;
@@ -1396,10 +1399,10 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
                 st = HALDA_STATUS_OPTIMAL;
                 nl = n;
                 if (lane < M) put_xc(A, inst, M, lane, wl, n, sl, z, me);
-                if (lane == 0 && (A.out.x || A.out.c)) {
+                if (lane == 0 && (A.outs & kOutXC)) {
                     const int64_t at = xc_at(A, inst);
-                    if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
-                    if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                    if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
                 }
             } else {
                 st = kSlotFlagged;  // a greedy fallback: the 64-lane table launch
@@ -1423,7 +1426,14 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
                 int64_t nodes = 0;
                 table_pass<S>(src, w, I, lane);
                 wave_sync();
-                const int feas = dp_pass_lanes(w, I, sg, nodes);
+#ifdef HALDA_STAMPS
+                t_rec[1] = __builtin_amdgcn_s_memtime();
+#endif
+                const int feas = dp_pass_lanes(w, I, sg, nodes, t_rec + 4);
+#ifdef HALDA_STAMPS
+                t_rec[2] = __builtin_amdgcn_s_memtime();
+                t_rec[3] = (unsigned long long)nodes;
+#endif
                 if (feas < 0) {
                     st = kSlotFlagged;  // a leaf the incremental scan does not take
                 } else if (!feas) {
@@ -1445,10 +1455,10 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
                     obj = obj + kappa;
                     st = HALDA_STATUS_OPTIMAL;
                     nl = n;
-                    if (lane == 0 && (A.out.x || A.out.c)) {
+                    if (lane == 0 && (A.outs & kOutXC)) {
                         const int64_t at = xc_at(A, inst);
-                        if (at >= 0 && A.out.x) A.out.x[at + 7 * M] = hmax;
-                        if (at >= 0 && A.out.c) A.out.c[at + 7 * M] = kc;
+                        if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
                     }
                 }
             }
@@ -1458,15 +1468,15 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
         flag_fleet(A, f, lane);
     } else {
         if (lane == 0) {
-            if (A.out.obj_by_k) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
-            if (A.out.status) A.out.status[inst] = st;
+            if (A.outs & kOutObk) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.outs & kOutSt) A.out.status[inst] = st;
         }
-        if (A.xz && st != HALDA_STATUS_OPTIMAL && (A.out.x || A.out.c)) {  // x / c of a non-optimal instance
+        if ((A.outs & kOutXZ) && st != HALDA_STATUS_OPTIMAL && (A.outs & kOutXC)) {  // x / c of a non-optimal instance
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = lane; cc < 7 * M + 1; cc += S) {
-                    if (A.out.x) A.out.x[at + cc] = 0.0;
-                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
                 }
         }
     }
@@ -1506,14 +1516,14 @@ __device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const 
         if (slot) continue;
         const int64_t inst = int64_t(f) * A.n_k + jj;
         const int st = !(A.Ws[jj] < 1000000) ? HALDA_STATUS_UNSUPPORTED : HALDA_STATUS_INFEASIBLE;
-        if (A.out.obj_by_k) A.out.obj_by_k[inst] = kInf;
-        if (A.out.status) A.out.status[inst] = st;
-        if (A.xz && (A.out.x || A.out.c)) {
+        if (A.outs & kOutObk) A.out.obj_by_k[inst] = kInf;
+        if (A.outs & kOutSt) A.out.status[inst] = st;
+        if ((A.outs & kOutXZ) && (A.outs & kOutXC)) {
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = 0; cc < 7 * M + 1; ++cc) {
-                    if (A.out.x) A.out.x[at + cc] = 0.0;
-                    if (A.out.c) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
                 }
         }
     }
@@ -1548,9 +1558,14 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         w.G = reinterpret_cast<double *>(base);
         w.H = reinterpret_cast<double *>(base + tb);
         w.st0 = reinterpret_cast<int *>(base + 2 * tb);
-        unsigned long long t_rec = 0;
-        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q, &t_rec);
-        HALDA_KSTAMPW(1, t_rec);
+        unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
+        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q, t_rec);
+        HALDA_KSTAMPW(1, t_rec[0]);
+        HALDA_KSTAMPW(6, t_rec[1]);
+        HALDA_KSTAMPW(7, t_rec[2]);
+        HALDA_KSTAMPW(8, t_rec[3]);
+        HALDA_KSTAMPW(9, t_rec[4]);
+        HALDA_KSTAMPW(10, t_rec[5]);
     }
     HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
     __syncthreads();

@@ -107,16 +107,23 @@ def b_cio_b(dev: DeviceProfile, model: ModelProfile) -> float:
     return ((model.b_in / model.V) + model.b_out) * (1.0 if dev.is_head else 0.0) + dev.c_cpu
 
 
+_CASE = {"mac_no_metal": 1, "mac_metal": 2}
+
+
 def classify_device_case(dev: DeviceProfile) -> int:
     """1 = macOS without Metal, 2 = macOS with Metal, 3 = everything else."""
-    return {"mac_no_metal": 1, "mac_metal": 2}.get(dev.os_type, 3)
+    return _CASE.get(dev.os_type, 3)
 
 
 def assign_sets(devs: List[DeviceProfile]) -> Dict[str, List[int]]:
-    sets: Dict[str, List[int]] = {"M1": [], "M2": [], "M3": []}
+    m1: List[int] = []
+    m2: List[int] = []
+    m3: List[int] = []
+    case = _CASE.get
     for i, d in enumerate(devs):
-        sets[f"M{classify_device_case(d)}"].append(i)
-    return sets
+        c = case(d.os_type, 3)
+        (m1 if c == 1 else m2 if c == 2 else m3).append(i)
+    return {"M1": m1, "M2": m2, "M3": m3}
 
 
 def objective_vectors(devs: List[DeviceProfile], model: ModelProfile, sets: Dict[str, List[int]],

@@ -225,10 +225,16 @@ def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) 
     off = np.empty(nf + 1, np.int64)
     heads = np.empty(nf, np.int64)
     _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, i64, u8, off, heads)
-    t = FleetTable(dev_off=off, os_class=u8[0], flags=u8[1], **{f: f64[j] for j, f in enumerate(F64_FIELDS)},
-                   **{f: i64[j] for j, f in enumerate(I64_FIELDS)})
-    t._blocks = (off, u8, f64, i64)  # FleetTable.check ran in the packer
-    t._heads = heads                   # kappa's head of each fleet (global device index)
+    # the dataclass's fields set directly (no per-field __setattr__), then the packed blocks they view
+    t = object.__new__(FleetTable)
+    d = t.__dict__
+    d["dev_off"], d["os_class"], d["flags"] = off, u8[0], u8[1]
+    for j, f in enumerate(F64_FIELDS):
+        d[f] = f64[j]
+    for j, f in enumerate(I64_FIELDS):
+        d[f] = i64[j]
+    d["_blocks"] = (off, u8, f64, i64)  # FleetTable.check ran in the packer
+    d["_heads"] = heads                  # kappa's head of each fleet (global device index)
     return t
 
 

@@ -92,7 +92,7 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                 t_comm, xi_sum, kappa = offsets
                 obj = float(c.dot(x)) + t_comm + xi_sum + kappa
                 wn = np.rint(x[:2 * M]).astype(np.int64).tolist()  # int(round(v)): both round half to even
-                r = ILPResult(k=k, w=wn[:M], n=wn[M:], obj_value=obj)
+                r = ILPResult.model_construct(k=k, w=wn[:M], n=wn[M:], obj_value=obj)  # fields already typed
             elif st != STATUS_INFEASIBLE:
                 raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
                                    "the lowered MILP does not have the HALDA structure")
@@ -131,8 +131,8 @@ def halda_solve(
     best = _pick(per_k)
     if best is None:
         raise RuntimeError("No feasible MILP found for any k this round.")
-    result = HALDAResult(w=list(best.w), n=list(best.n), k=best.k, obj_value=best.obj_value,
-                         sets={k: list(v) for k, v in sets.items()})
+    result = HALDAResult.model_construct(w=list(best.w), n=list(best.n), k=best.k, obj_value=best.obj_value,
+                                         sets={k: list(v) for k, v in sets.items()})
     if plot:
         from .plotter import plot_k_curve
 

@@ -42,7 +42,7 @@ def main():
     slots = [k for k in KS if 80 // k >= args.M]
     groups = (args.fleets + 3) // 4
     n = groups * len(slots)
-    K = 10
+    K = 12
     buf = (ctypes.c_ulonglong * (K * n))()
     lib.halda_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.halda_debug_stamps(buf, n)
@@ -53,6 +53,13 @@ def main():
         s = st[:, j]
         print(f"  k={k:3d} records {np.percentile(s[:, 1] - s[:, 0], q)}  solve {np.percentile(s[:, 2] - s[:, 1], q)}"
               f"  barrier wait {np.percentile(s[:, 3] - s[:, 2], q)}")
+    for j, k in enumerate(slots):
+        s = st[:, j]
+        if (s[:, 6] > 0).all():
+            print(f"  k={k:3d} tables {np.percentile(s[:, 6] - s[:, 1], q)}  leaf scan {np.percentile(s[:, 9] - s[:, 6], q)}"
+                  f"  phase-0 greedy {np.percentile(s[:, 10] - s[:, 9], q)}  threshold scan "
+                  f"{np.percentile(s[:, 7] - s[:, 10], q)}  output {np.percentile(s[:, 2] - s[:, 7], q)}  "
+                  f"scan events (segment 0) {np.percentile(s[:, 8], q)}")
     s0 = st[:, 0]
     print(f"  pick (slot 0) {np.percentile(s0[:, 4] - s0[:, 3], q)}")
     life = st[:, :, 4].max(axis=1) - st[:, :, 0].min(axis=1)

@@ -32,7 +32,7 @@ def main():
         res = ctx.solve(batch)
     lib = load_library()
     n = min(batch.n_inst, 65536)
-    K = 10  # kStamps in halda.hip
+    K = 12  # kStamps in halda.hip
     buf = (ctypes.c_ulonglong * (K * n))()
     lib.halda_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     got = lib.halda_debug_stamps(buf, n)

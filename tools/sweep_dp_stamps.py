@@ -32,7 +32,7 @@ def main():
     table = fleet_table(bench.build_fleets(range(args.fleets), args.M), model)
     dt = DeviceFleetTable(table, model, KS, 0.5, dev, want_per_k=True)
     lib = load_library()
-    K = 10
+    K = 12
     n = min(args.fleets * len(KS), 65536)
     buf = (ctypes.c_ulonglong * (K * n))()
     lib.halda_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -35,7 +35,7 @@ def main():
         dt.launch(ctx, stream.cuda_stream)
     torch.cuda.synchronize(dev)
     lib = load_library()
-    K = 10
+    K = 12
     n = args.fleets
     buf = (ctypes.c_ulonglong * (K * n))()
     lib.halda_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -6,7 +6,7 @@ profiled), e.g. via profiles/run_valu.sh:
   python tools/valu_stamp.py r03 c3=gpurun_out/valu_c3/run_counter_collection.csv \
                                  c2=gpurun_out/valu_c2/run_counter_collection.csv
 
-Writes profiles/<R>_valu.json: {"libhalda_sha256": ..., "workloads": {"c3": {kernel: {...}}, ...}}
+Writes gpurun_out/<R>_valu.json (copied to profiles/ afterwards): {"libhalda_sha256": ..., "workloads": {"c3": {kernel: {...}}, ...}}
 with, per kernel, the largest launch's SQ_INSTS_VALU / SQ_WAVES (valu_per_wave), SQ_WAVES (waves),
 SQ_WAIT_ANY / SQ_WAVE_CYCLES (wait_any_frac), SALU and LDS instructions per wave. bench.py reads
 it for the VALU-issue roof only when the hash matches the library it loads.
@@ -69,7 +69,9 @@ def main():
     for arg in sys.argv[2:]:
         name, path = arg.split("=", 1)
         res["workloads"][name] = summarise(path)
-    dst = REPO / "profiles" / f"{R}_valu.json"
+    # written under gpurun_out/ on the GPU box (merged back), then copied to profiles/ by the builder
+    dst = REPO / "gpurun_out" / f"{R}_valu.json"
+    dst.parent.mkdir(exist_ok=True)
     dst.write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res))
 
