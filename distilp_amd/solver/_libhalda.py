@@ -87,6 +87,24 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _torch_runtime_first() -> None:
+    """PyTorch-ROCm bundles its own HIP runtime, libhalda links /opt/rocm's: when libhalda's
+    initialises the GPU first, torch's then finds no device in this process ("No HIP GPUs are
+    available"; the other order works, tools/probe_runtime_order.py). So when torch is already
+    imported, its runtime is initialised before libhalda is loaded. (A program that imports torch only
+    after its first libhalda call must initialise torch's CUDA itself first: INTEGRATION.md.)"""
+    import sys
+
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return
+    try:
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except Exception:  # noqa: BLE001 -- no GPU / CPU-only torch: nothing to order
+        pass
+
+
 def load_library(path: Path | str | None = None):
     """dlopen libhalda and declare the prototypes. Raises HaldaUnavailable if absent."""
     global _lib
@@ -94,6 +112,7 @@ def load_library(path: Path | str | None = None):
         if _lib is not None and path is None:
             return _lib
         p = Path(path) if path is not None else LIB_PATH
+        _torch_runtime_first()
         if not p.exists():
             raise HaldaUnavailable(f"{p} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                                    "or `make -C distilp_amd/csrc`")

@@ -15,6 +15,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU tests")
 
 
+def pytest_collection_modifyitems(config, items):
+    # GPU runs: PyTorch's bundled HIP runtime must initialise before libhalda's (see
+    # distilp_amd.solver._libhalda._torch_runtime_first), whichever test file comes first
+    if any(item.get_closest_marker("gpu") for item in items):
+        import torch  # noqa: F401
+
+
 def load_json(name):
     return json.loads((GOLDEN / name).read_text())
 

@@ -184,3 +184,20 @@ def test_batch_api_equals_halda_solve_bits(llama_online_model):
     assert all(r is not None and r.k in (1, 3) for r in out)
     with pytest.raises(ZeroDivisionError):
         halda_solve_batch(fleets[:2], llama_online_model, k_candidates=[0, 1], kv_bits="4bit")
+
+
+def test_torch_still_sees_the_gpu_after_libhalda():
+    """PyTorch-ROCm bundles its own HIP runtime: libhalda initialises torch's first when torch is
+    imported (tools/probe_runtime_order.py shows the failure the other way round), so a process that
+    imported torch, then solved with libhalda, can still use torch's device (a fresh subprocess, so
+    that nothing initialised either runtime before)."""
+    import subprocess
+    import sys
+
+    from .conftest import REPO
+
+    code = ("import sys; sys.path.insert(0, '.'); import torch; "
+            "from distilp_amd.solver._libhalda import get_context; get_context(0); "
+            "x = torch.ones(8, device='cuda'); print(float(x.sum()))")
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(REPO), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and r.stdout.strip().endswith("8.0"), r.stderr[-2000:]
