@@ -932,19 +932,9 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
         typename Src::Rec d;
         src.load(d, w, min(i, I.M - 1));
         if (i < I.M) {
-            // 16-lane segments (the k-slot / segment sweeps, one device per lane): two independent
-            // chains per lane, e in [0, h) and [h, R1), advanced in the same iteration (the second
-            // starts with a full split search, as a stretch of the P-lane layout above: the same least
-            // minimisers, so the same G and H); their dependent split / cycle-time arithmetic
-            // interleaves instead of one chain of R1 entries. (The 64-lane kernels keep one chain: their
-            // register budget is spent elsewhere.)
-            const int h = S == 16 ? (I.R1 + 1) / 2 : I.R1;
-            int na = 0, nb = 0;
-            bool ha = false, hb = false;
-            for (int e = 0; e < h; ++e) {
-                table_entry(d, w, I, i, e, na, ha);
-                if (S == 16 && h + e < I.R1) table_entry(d, w, I, i, h + e, nb, hb);
-            }
+            int n = 0;
+            bool have = false;
+            for (int e = 0; e < I.R1; ++e) table_entry(d, w, I, i, e, n, have);
         }
     }
 }

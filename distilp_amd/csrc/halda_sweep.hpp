@@ -1336,25 +1336,100 @@ struct SlotArgs {
 
 // One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
 // its w / n candidate).
-__device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tabcap, const WaveCtx &w,
-                            const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec) {
+// One fleet of a k-slot workgroup, in registers: its extent, this lane's device record and the
+// objective constants (every wave of the workgroup builds the same, from one round of field loads).
+struct KslotFleet {
+    int64_t d0;
+    int M;
+    FieldRec me;
+    double tsum, xsum, kappa;
+    bool anybad;
+};
+
+__device__ inline KslotFleet kslot_records(const SweepArgs &A, int f, const Seg<kSegLanes> &sg) {
+    KslotFleet fd;
+    const int lane = sg.sl;
+    const halda_fleets &F = A.F;
+    fd.d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
+    fd.M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - fd.d0);
+    const DevFields mf = load_fields(F, fd.d0 + (lane < fd.M ? lane : 0));
+    int bad = 0;
+    fd.me = field_rec(A.Mo, mf, bad);
+    bad = lane < fd.M ? bad : 0;
+    fleet_offsets_regs(A.Mo, mf, fd.M, sg, fd.tsum, fd.xsum, fd.kappa);
+    fd.anybad = sg.any(bad != 0);
+    return fd;
+}
+
+// The (fleet, k_j) instance solves through the tables + threshold scan (not the register greedy /
+// forced split, not flagged): the same conditions sweep_kslot's branches test.
+__device__ inline bool kslot_uses_tables(const KslotFleet &fd, int k, int W, int r1cap, int tabcap, int mmax) {
+    if (!(W < 1000000) || fd.M > W || fd.anybad || k == 1 || W == fd.M || fd.M < 2) return false;
+    const int R1 = W - fd.M + 1;
+    return fd.M <= mmax && R1 <= r1cap && int64_t(fd.M) * odd_stride(R1) <= tabcap;
+}
+
+// Slot p's LDS slice of this segment.
+__device__ inline WaveCtx kslot_ctx(const SweepArgs &A, const SlotArgs &SA, int p, unsigned char *smem, int seg) {
+    const int tab = SA.tab[p];
+    const int64_t tb = align16(int64_t(tab) * 8);
+    unsigned char *base = smem + SA.off[p] + int64_t(seg) * seg_slice_bytes(A.mmax, tab);
+    WaveCtx w = {};
+    w.G = reinterpret_cast<double *>(base);
+    w.H = reinterpret_cast<double *>(base + tb);
+    w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+    return w;
+}
+
+// Phase B of the k-slot workgroup: every wave builds an equal share of ALL the slots' k > 1 tables
+// (the (slot, entry) pairs in slot order, cut into n_slot contiguous stretches; lane = device; each
+// stretch starts with a full split search, the same least minimisers as one chain, so the same
+// tables), instead of each k > 1 wave building its own while the W = M / k = 1 waves idle at the
+// barrier: the longest wave's dependent chain loses its table pass.
+__device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, const KslotFleet &fd,
+                             const Seg<kSegLanes> &sg, unsigned char *smem, int seg) {
+    const int lane = sg.sl;
+    int total = 0;
+    for (int p = 0; p < SA.n_slot; ++p) total += SA.tab[p] > 0 ? SA.r1[p] : 0;
+    const int lo = q * total / SA.n_slot, hi = (q + 1) * total / SA.n_slot;
+    int base = 0;
+    for (int p = 0; p < SA.n_slot; ++p) {
+        if (SA.tab[p] <= 0) continue;
+        const int b0 = base;
+        base += SA.r1[p];
+        const int a = max(lo, b0) - b0, b = min(hi, base) - b0;
+        if (a >= b) continue;
+        const int k = A.ks[SA.j[p]], W = A.Ws[SA.j[p]];
+        if (!kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) continue;
+        Inst I = {};
+        I.M = fd.M;
+        I.W = W;
+        I.Wd = double(W);
+        I.kc = double(k - 1);
+        I.iC = 7 * fd.M;
+        I.R1 = W - fd.M + 1;
+        I.RS = odd_stride(I.R1);
+        const WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
+        FieldRec rec = fd.me;
+        rec.W = W;
+        if (lane < fd.M) {
+            int n = 0;
+            bool have = false;
+            for (int e = a; e < min(b, I.R1); ++e) table_entry(rec, w, I, lane, e, n, have);
+        }
+    }
+}
+
+__device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int j, int r1cap, int tabcap,
+                            const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec) {
     using SG = Seg<kSegLanes>;
     constexpr int S = SG::S;
     const int lane = sg.sl;
-    const halda_model &Mo = A.Mo;
-    const halda_fleets &F = A.F;
-    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
-    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
-    const DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
-    int bad = 0;
-    FieldRec me = field_rec(Mo, mf, bad);
-    bad = lane < M ? bad : 0;
-    double tsum, xsum, kappa;
-    fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
-    const bool anybad = sg.any(bad != 0);
-#ifdef HALDA_STAMPS
-    t_rec[0] = __builtin_amdgcn_s_memtime();
-#else
+    const int M = fd.M;
+    FieldRec me = fd.me;
+    const double tsum = fd.tsum, xsum = fd.xsum, kappa = fd.kappa;
+    const bool anybad = fd.anybad;
+#ifndef HALDA_STAMPS
     (void)t_rec;
 #endif
     const int k = A.ks[j], W = A.Ws[j];
@@ -1422,13 +1497,8 @@ __device__ void sweep_kslot(const SweepArgs &A, int f, int j, int r1cap, int tab
             if (M > A.mmax || I.R1 > r1cap || int64_t(M) * I.RS > tabcap) {
                 st = kSlotFlagged;  // beyond the slot's slice
             } else {
-                const FieldSrc src{&A.Mo, &A.F, &me, d0, W, sg.base};
+                // the tables were built by the whole workgroup (kslot_tables, before the barrier)
                 int64_t nodes = 0;
-                table_pass<S>(src, w, I, lane);
-                wave_sync();
-#ifdef HALDA_STAMPS
-                t_rec[1] = __builtin_amdgcn_s_memtime();
-#endif
                 const int feas = dp_pass_lanes(w, I, sg, nodes, t_rec + 4);
 #ifdef HALDA_STAMPS
                 t_rec[2] = __builtin_amdgcn_s_memtime();
@@ -1551,17 +1621,16 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     HALDA_KSTAMPW(5, __builtin_amdgcn_s_memrealtime());
     {
-        const int tab = SA.tab[q];
-        const int64_t tb = align16(int64_t(tab) * 8);
-        unsigned char *base = smem + SA.off[q] + int64_t(seg) * seg_slice_bytes(A.mmax, tab);
-        WaveCtx w = {};
-        w.G = reinterpret_cast<double *>(base);
-        w.H = reinterpret_cast<double *>(base + tb);
-        w.st0 = reinterpret_cast<int *>(base + 2 * tb);
+        KslotFleet fd = {};
+        if (f < nf) fd = kslot_records(A, int(f), sg);
+        HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
+        if (f < nf) kslot_tables(A, SA, q, fd, sg, smem, seg);
+        HALDA_KSTAMPW(6, __builtin_amdgcn_s_memtime());
+        __syncthreads();  // every slot's tables are complete
+        HALDA_KSTAMPW(11, __builtin_amdgcn_s_memtime());
+        const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
-        if (f < nf) sweep_kslot(A, int(f), SA.j[q], SA.r1[q], tab, w, sg, pick + seg * SA.n_slot + q, t_rec);
-        HALDA_KSTAMPW(1, t_rec[0]);
-        HALDA_KSTAMPW(6, t_rec[1]);
+        if (f < nf) sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec);
         HALDA_KSTAMPW(7, t_rec[2]);
         HALDA_KSTAMPW(8, t_rec[3]);
         HALDA_KSTAMPW(9, t_rec[4]);

@@ -51,12 +51,13 @@ def main():
     print(f"{groups} workgroups x {len(slots)} k-slots {slots}; shader-clock cycles, percentiles {q}")
     for j, k in enumerate(slots):
         s = st[:, j]
-        print(f"  k={k:3d} records {np.percentile(s[:, 1] - s[:, 0], q)}  solve {np.percentile(s[:, 2] - s[:, 1], q)}"
+        print(f"  k={k:3d} records {np.percentile(s[:, 1] - s[:, 0], q)}  table share {np.percentile(s[:, 6] - s[:, 1], q)}"
+              f"  wait for tables {np.percentile(s[:, 11] - s[:, 6], q)}  solve {np.percentile(s[:, 2] - s[:, 11], q)}"
               f"  barrier wait {np.percentile(s[:, 3] - s[:, 2], q)}")
     for j, k in enumerate(slots):
         s = st[:, j]
-        if (s[:, 6] > 0).all():
-            print(f"  k={k:3d} tables {np.percentile(s[:, 6] - s[:, 1], q)}  leaf scan {np.percentile(s[:, 9] - s[:, 6], q)}"
+        if (s[:, 9] > 0).all():
+            print(f"  k={k:3d} leaf scan {np.percentile(s[:, 9] - s[:, 11], q)}"
                   f"  phase-0 greedy {np.percentile(s[:, 10] - s[:, 9], q)}  threshold scan "
                   f"{np.percentile(s[:, 7] - s[:, 10], q)}  output {np.percentile(s[:, 2] - s[:, 7], q)}  "
                   f"scan events (segment 0) {np.percentile(s[:, 8], q)}")
