@@ -16,6 +16,7 @@
 #define PY_SSIZE_T_CLEAN
 #define _GNU_SOURCE
 #include <Python.h>
+#include <math.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdint.h>
@@ -526,8 +527,120 @@ done:
     return ret;
 }
 
+/* results(cls, x, row, k, obj, off, os_class) -> list
+ * The HALDAResult of every fleet of a solved batch (halda._batch_on_gpu), built without Python
+ * bytecode per fleet: fleet f's winner row starts at x[row[f]] (-1: no feasible k -> None), w = the
+ * rint of its first M entries and n of the next M (int(round(v)): both round half to even), k[f],
+ * obj[f], sets = the device indices of class 1 / 2 / 3 in device order (assign_sets,
+ * dense_common.py:149-167). Each object is what cls.model_construct(w=..., n=..., k=..., obj_value=...,
+ * sets=...) gives: the field dict, its own fields-set, no extra / private state. */
+static PyObject *s_dict, *s_fset, *s_extra, *s_priv, *s_w, *s_n, *s_k, *s_obj, *s_sets, *s_m[3];
+
+static PyObject *int_list(const double *v, Py_ssize_t M) {
+    PyObject *l = PyList_New(M);
+    if (!l) return NULL;
+    for (Py_ssize_t i = 0; i < M; ++i) {
+        PyObject *o = PyLong_FromDouble(nearbyint(v[i]));
+        if (!o) { Py_DECREF(l); return NULL; }
+        PyList_SET_ITEM(l, i, o);
+    }
+    return l;
+}
+
+static PyObject *one_result(PyTypeObject *cls, PyObject *noargs, const double *xr, Py_ssize_t M, long long k, double obj,
+                            const uint8_t *cls_row) {
+    PyObject *d = NULL, *o = NULL, *fs = NULL, *sets = NULL, *v = NULL;
+    if (!(d = PyDict_New())) goto fail;
+    if (!(v = int_list(xr, M)) || PyDict_SetItem(d, s_w, v)) goto fail;
+    Py_CLEAR(v);
+    if (!(v = int_list(xr + M, M)) || PyDict_SetItem(d, s_n, v)) goto fail;
+    Py_CLEAR(v);
+    if (!(v = PyLong_FromLongLong(k)) || PyDict_SetItem(d, s_k, v)) goto fail;
+    Py_CLEAR(v);
+    if (!(v = PyFloat_FromDouble(obj)) || PyDict_SetItem(d, s_obj, v)) goto fail;
+    Py_CLEAR(v);
+    if (!(sets = PyDict_New())) goto fail;
+    for (int s = 1; s <= 3; ++s) {
+        Py_ssize_t cnt = 0;
+        for (Py_ssize_t i = 0; i < M; ++i) cnt += cls_row[i] == s;
+        if (!(v = PyList_New(cnt))) goto fail;
+        for (Py_ssize_t i = 0, j = 0; i < M; ++i)
+            if (cls_row[i] == s) {
+                PyObject *ix = PyLong_FromSsize_t(i);
+                if (!ix) goto fail;
+                PyList_SET_ITEM(v, j++, ix);
+            }
+        if (PyDict_SetItem(sets, s_m[s - 1], v)) goto fail;
+        Py_CLEAR(v);
+    }
+    if (PyDict_SetItem(d, s_sets, sets)) goto fail;
+    Py_CLEAR(sets);
+    if (!(fs = PySet_New(NULL))) goto fail;
+    PyObject *names[5] = {s_w, s_n, s_k, s_obj, s_sets};
+    for (int a = 0; a < 5; ++a)
+        if (PySet_Add(fs, names[a])) goto fail;
+    /* object.__new__(cls) and object.__setattr__ of the four slots, as model_construct does */
+    if (!(o = PyBaseObject_Type.tp_new(cls, noargs, NULL))) goto fail;
+    if (PyObject_GenericSetAttr(o, s_dict, d) || PyObject_GenericSetAttr(o, s_fset, fs) ||
+        PyObject_GenericSetAttr(o, s_extra, Py_None) || PyObject_GenericSetAttr(o, s_priv, Py_None))
+        goto fail;
+    Py_DECREF(d);
+    Py_DECREF(fs);
+    return o;
+fail:
+    Py_XDECREF(d);
+    Py_XDECREF(o);
+    Py_XDECREF(fs);
+    Py_XDECREF(sets);
+    Py_XDECREF(v);
+    return NULL;
+}
+
+static PyObject *results(PyObject *self, PyObject *args) {
+    (void)self;
+    PyObject *cls;
+    Py_buffer bx, br, bk, bo, boff, bc;
+    if (!PyArg_ParseTuple(args, "Oy*y*y*y*y*y*", &cls, &bx, &br, &bk, &bo, &boff, &bc)) return NULL;
+    PyObject *ret = NULL, *noargs = NULL;
+    const Py_ssize_t nf = br.len / 8, nx = bx.len / 8, nd = bc.len;
+    if (!PyType_Check(cls) || bk.len < 8 * nf || bo.len < 8 * nf || boff.len < 8 * (nf + 1)) {
+        PyErr_SetString(PyExc_ValueError, "results: bad arguments");
+        goto done;
+    }
+    if (!(noargs = PyTuple_New(0)) || !(ret = PyList_New(nf))) goto done;
+    const double *x = (const double *)bx.buf, *obj = (const double *)bo.buf;
+    const int64_t *row = (const int64_t *)br.buf, *kk = (const int64_t *)bk.buf, *off = (const int64_t *)boff.buf;
+    const uint8_t *cl = (const uint8_t *)bc.buf;
+    for (Py_ssize_t f = 0; f < nf; ++f) {
+        const int64_t a = off[f], M = off[f + 1] - off[f], r = row[f];
+        PyObject *o;
+        if (r < 0) {
+            Py_INCREF(Py_None);
+            o = Py_None;
+        } else if (a < 0 || M < 0 || a + M > nd || r + 2 * M > nx) {
+            PyErr_SetString(PyExc_ValueError, "results: row or device range out of bounds");
+            Py_CLEAR(ret);
+            goto done;
+        } else if (!(o = one_result((PyTypeObject *)cls, noargs, x + r, M, kk[f], obj[f], cl + a))) {
+            Py_CLEAR(ret);
+            goto done;
+        }
+        PyList_SET_ITEM(ret, f, o);
+    }
+done:
+    Py_XDECREF(noargs);
+    PyBuffer_Release(&bx);
+    PyBuffer_Release(&br);
+    PyBuffer_Release(&bk);
+    PyBuffer_Release(&bo);
+    PyBuffer_Release(&boff);
+    PyBuffer_Release(&bc);
+    return ret;
+}
+
 static PyMethodDef methods[] = {{"pack", pack, METH_VARARGS, "Pack fleets of DeviceProfile into the fleet table."},
                                 {"consts", consts, METH_VARARGS, "Per-fleet obj_value constants of a packed table."},
+                                {"results", results, METH_VARARGS, "HALDAResult per fleet of a solved batch."},
                                 {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_fleetpack", NULL, -1, methods, NULL, NULL, NULL, NULL};
@@ -536,5 +649,10 @@ PyMODINIT_FUNC PyInit__fleetpack(void) {
 #define MAKE(n) if (!(k_##n = PyUnicode_InternFromString(#n)) || (h_##n = PyObject_Hash(k_##n)) == -1) return NULL;
     KEYS(MAKE)
 #undef MAKE
+#define STR(v, s) if (!(v = PyUnicode_InternFromString(s))) return NULL;
+    STR(s_dict, "__dict__") STR(s_fset, "__pydantic_fields_set__") STR(s_extra, "__pydantic_extra__")
+    STR(s_priv, "__pydantic_private__") STR(s_w, "w") STR(s_n, "n") STR(s_k, "k") STR(s_obj, "obj_value")
+    STR(s_sets, "sets") STR(s_m[0], "M1") STR(s_m[1], "M2") STR(s_m[2], "M3")
+#undef STR
     return PyModule_Create(&mod);
 }

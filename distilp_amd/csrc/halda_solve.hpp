@@ -1081,22 +1081,32 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     int lo = R1, hi = -1, cnt = 0;
     bool ok = true, mono = true;
     double prev = kInf, dprev = -kInf, hprev = -kInf;
+    // the row in chunks of 8 entries: the chunk's 16 LDS reads are issued together, then the entries
+    // are scanned in registers with selects (one LDS round trip per chunk, not per entry)
     if (act)
-#pragma unroll 4
-        for (int e = 0; e < R1; ++e) {
-            const double g = G[e], h = H[e];
-            if (g < kInf) {
-                if (cnt > 0) {
-                    const double d = g - prev;
-                    ok = ok && (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
-                    dprev = d;
-                }
-                mono = mono && h >= hprev;
-                hprev = h;
-                lo = min(lo, e);
-                hi = e;
-                prev = g;
-                ++cnt;
+        for (int e0 = 0; e0 < R1; e0 += 8) {
+            double gc[8], hc[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int e = min(e0 + t, R1 - 1);
+                gc[t] = G[e];
+                hc[t] = H[e];
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int e = e0 + t;
+                const double g = gc[t], h = hc[t];
+                const bool fin = e < R1 && g < kInf;
+                const double d = g - prev;
+                const bool conv = (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
+                ok = (fin && cnt > 0) ? ok && conv : ok;
+                dprev = (fin && cnt > 0) ? d : dprev;
+                mono = fin ? mono && h >= hprev : mono;
+                hprev = fin ? h : hprev;
+                lo = fin ? min(lo, e) : lo;
+                hi = fin ? e : hi;
+                prev = fin ? g : prev;
+                cnt += fin ? 1 : 0;
             }
         }
     if (sg.any(act && (!ok || !mono))) return -1;

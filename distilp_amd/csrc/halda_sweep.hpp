@@ -1619,7 +1619,11 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     const int64_t f = int64_t(blockIdx.x) * kPer + seg;
     SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
-    HALDA_KSTAMPW(5, __builtin_amdgcn_s_memrealtime());
+    // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
+    // XCC_ID[3:0] above
+    HALDA_KSTAMPW(5, (__builtin_amdgcn_s_memrealtime() & ((1ull << 40) - 1)) |
+                         (uint64_t(__builtin_amdgcn_s_getreg((15 << 11) | 4)) << 40) |
+                         (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20)) << 56));
     {
         KslotFleet fd = {};
         if (f < nf) fd = kslot_records(A, int(f), sg);

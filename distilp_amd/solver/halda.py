@@ -32,7 +32,7 @@ import numpy as np
 from ..common import DeviceProfile, ModelProfile
 from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL
 from .coefficients import HALDAResult, ILPResult, assign_sets, kappa_constant, valid_factors_of_L
-from .fleets import fleet_constants, fleet_table, solve_table
+from .fleets import _PACKER, fleet_constants, fleet_table, solve_table
 from .lower import kv_bits_to_factor
 
 
@@ -172,21 +172,35 @@ def _batch_on_gpu(fleets: Sequence[List[DeviceProfile]], model: ModelProfile, Ks
     opt = st == STATUS_OPTIMAL
     obj = np.full((nf, nk), np.inf)
     xo = res.x_off.reshape(nf, nk)
-    for M in np.unique(sizes):  # one vectorised dot per row length N = 7 M + 1
+    ms = np.unique(sizes)
+    for M in ms:  # one vectorised dot per row length N = 7 M + 1
         N = 7 * int(M) + 1
         fi, ji = np.nonzero(opt & (sizes == M)[:, None])
         if len(fi) == 0:
             continue
-        idx = xo[fi, ji][:, None] + np.arange(N)[None, :]
-        cx = np.vecdot(res.c[idx], res.x[idx])
+        if len(ms) == 1:
+            # one fleet size: the open instances' rows lie back to back from 0 (open_x_offsets), so the
+            # rows are a strided view of x / c, no gather
+            n_open = int((xo >= 0).sum())
+            X, C = res.x[:n_open * N].reshape(n_open, N), res.c[:n_open * N].reshape(n_open, N)
+            cx = np.vecdot(C, X)[xo[fi, ji] // N]
+        else:
+            idx = xo[fi, ji][:, None] + np.arange(N)[None, :]
+            cx = np.vecdot(res.c[idx], res.x[idx])
         obj[fi, ji] = ((cx + t_sum[fi]) + x_sum[fi]) + kappa[fi]
     feas = opt.any(axis=1)
     bj = np.argmin(obj, axis=1)  # the first minimum: ascending k, strict "<"
     best_obj = obj[np.arange(nf), bj]
     best_a = xo[np.arange(nf), bj]
+    if _PACKER is not None and hasattr(_PACKER, "results"):
+        # every HALDAResult built in C (w, n = rint of the winner's x; sets from the device classes)
+        row = np.where(feas, best_a, -1).astype(np.int64)
+        kk = np.asarray(pos, np.int64)[bj]
+        return _PACKER.results(HALDAResult, res.x, row, kk, np.ascontiguousarray(best_obj), table.dev_off,
+                               np.ascontiguousarray(table.os_class))
     out: List[Optional[HALDAResult]] = [None] * nf
     cls = table.os_class
-    for M in np.unique(sizes):
+    for M in ms:
         M = int(M)
         fs = np.flatnonzero(feas & (sizes == M))
         if len(fs) == 0:

@@ -295,3 +295,62 @@ def test_open_x_offsets_layout(llama_online_model):
                 assert off[f, j] == -1
     assert (off >= 0).sum() == sum(sum(80 // k >= M for k in ks) for M in sizes)
     assert np.array_equal(open_x_offsets(t, llama_online_model, []), np.zeros(0, np.int64))
+
+
+@pytest.mark.parametrize("sizes", [[64] * 40, [16, 64, 3, 1, 40, 16, 7]])
+def test_batch_results_c_builder_equals_python(llama_online_model, monkeypatch, sizes):
+    """halda._batch_on_gpu's host half on a stand-in GPU answer (solve_table replaced): the objectives
+    through the strided-row dot (one fleet size) or the gather (mixed sizes), and the HALDAResult list
+    built in C (_fleetpack.results) equal the Python construction (model_construct per fleet) field for
+    field -- w / n rounded half to even, k, obj_value, sets -- with None where no k is feasible; each
+    object owns its fields-set."""
+    import types
+
+    import numpy as np
+
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.solver import halda as H
+    from distilp_amd.solver.fleets import FleetSolve, fleet_table, open_x_offsets
+    from distilp_amd.synth import synth_fleet
+
+    m = llama_online_model
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(40 + s, M)] for s, M in enumerate(sizes)]
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    table = fleet_table(fleets, m)
+    xo = open_x_offsets(table, m, ks)
+    nf, nk = len(fleets), len(ks)
+    ext = int(np.max(xo + np.repeat(7 * table.sizes() + 1, nk)))
+    rng = np.random.default_rng(1)
+    st = np.where(xo.reshape(nf, nk) >= 0, 0, 2).astype(np.int32)
+    st[3 % nf, :] = 2  # a fleet without a feasible k
+    x = rng.integers(0, 9, 2 * ext).astype(np.float64) + np.where(rng.random(2 * ext) < 0.3, 0.5, 0.0)
+    x[ext:] = rng.normal(size=ext)
+    res = FleetSolve(best_k=None, obj_value=None, w=None, n=None, obj_by_k=None, status=st, ks=ks, x=x[:ext],
+                     c=x[ext:], x_off=xo)
+    monkeypatch.setattr(H, "solve_table", lambda *a, **k: res)
+    got = H._batch_on_gpu(fleets, m, ks, 0.5, 0)
+    monkeypatch.setattr(H, "_PACKER", types.SimpleNamespace())  # no `results`: the Python construction
+    want = H._batch_on_gpu(fleets, m, ks, 0.5, 0)
+    assert len(got) == len(want) == nf and got[3 % nf] is None and want[3 % nf] is None
+    for g, w in zip(got, want):
+        if w is None:
+            assert g is None
+            continue
+        assert type(g) is type(w) and g.model_dump() == w.model_dump() and g == w
+        assert all(type(v) is int for v in g.w + g.n) and type(g.k) is int and type(g.obj_value) is float
+        assert g.model_fields_set == w.model_fields_set
+    # the objective of every fleet against the reference's own formula on the same c and x
+    from distilp_amd.solver.fleets import fleet_constants
+
+    t_sum, x_sum, kap = fleet_constants(table, m)
+    sz = table.sizes()
+    for f, g in enumerate(got):
+        if g is None:
+            continue
+        N = 7 * int(sz[f]) + 1
+        objs = [float(res.c[xo[f * nk + j]:xo[f * nk + j] + N].dot(res.x[xo[f * nk + j]:xo[f * nk + j] + N]))
+                + t_sum[f] + x_sum[f] + kap[f] if st[f, j] == 0 else np.inf for j in range(nk)]
+        assert g.obj_value == min(objs) and g.k == ks[int(np.argmin(objs))], f
+    live = [g for g in got if g is not None]
+    live[0].k = 99
+    assert live[1].k != 99 and "k" in live[1].model_fields_set

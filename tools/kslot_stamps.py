@@ -65,8 +65,22 @@ def main():
     print(f"  pick (slot 0) {np.percentile(s0[:, 4] - s0[:, 3], q)}")
     life = st[:, :, 4].max(axis=1) - st[:, :, 0].min(axis=1)
     print(f"  workgroup life {np.percentile(life, q)}")
-    t0 = st[:, :, 5]
+    t0 = st[:, :, 5] & ((1 << 40) - 1)
     print(f"  wave start spread (10 ns ticks) {np.percentile(t0 - t0.min(), [0, 10, 50, 90, 100])}")
+    hw = (st[:, :, 5] >> 40) & 0xFFFF  # HW_ID[15:0]: wave slot [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]
+    xcc = (st[:, :, 5] >> 56) & 0xF
+    simd = (hw >> 4) & 3
+    for j, k in enumerate(slots):
+        print(f"  k={k:3d} waves per SIMD id {np.bincount(simd[:, j], minlength=4).tolist()}")
+    same = (simd[:, :, None] == simd[:, None, :]).sum(axis=(1, 2)) - len(slots)
+    print(f"  workgroups whose slot waves share a SIMD: {int((same > 0).sum())} of {groups}")
+    # chip-wide SIMD key (XCC, SE, SH, CU, SIMD): how many waves of each k-slot share one SIMD
+    key = (xcc << 16) | (hw >> 4)
+    for j, k in enumerate(slots):
+        _, cnt = np.unique(key[:, j], return_counts=True)
+        print(f"  k={k:3d} waves sharing one SIMD: {np.bincount(cnt).tolist()} (index = waves on the SIMD)")
+    _, cnt = np.unique(key.ravel(), return_counts=True)
+    print(f"  all slot waves per SIMD: {np.bincount(cnt).tolist()}; SIMDs used {len(cnt)}")
 
 
 if __name__ == "__main__":
