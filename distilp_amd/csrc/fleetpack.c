@@ -73,8 +73,9 @@ static int rate(PyObject *table, PyObject *Q, int fq, int *present, double *v) {
     return as_f64(b1, v);
 }
 
-/* ---------------------------------------------------------------- parallel pass
- * Large tables are packed by several threads while the calling thread holds the GIL and waits, so
+/* ---------------------------------------------------------------- fast (parallel) pass
+ * Large tables are packed by several threads while the calling thread holds the GIL and waits (small
+ * ones by the calling thread itself), so
  * no Python code runs and no object changes meanwhile. The workers only READ: borrowed instance
  * dicts (_PyObject_GetDictPtr), lookups by precomputed hash in str-keyed dicts
  * (_PyDict_GetItem_KnownHash: no error state, no Python code), and the values of exact float / int /
@@ -238,7 +239,7 @@ static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f
     (void)fout;
     const Py_ssize_t nf = PySequence_Fast_GET_SIZE(seq);
     int nt = pack_threads(nd);
-    if (nt < 1 || (nt == 1 && !getenv("HALDA_PACK_THREADS")) || !PyUnicode_CheckExact(Q)) return 0;
+    if (nt < 1 || !PyUnicode_CheckExact(Q)) return 0;
     const Py_hash_t hQ = PyObject_Hash(Q);
     if (hQ == -1) return -1;
     PyObject **devs = (PyObject **)malloc(sizeof(PyObject *) * (size_t)(nd > 0 ? nd : 1));
@@ -261,7 +262,11 @@ static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f
     Job jobs[64];
     volatile int bail = 0;
     int started = 0;
-    for (int t = 0; t < nt; ++t) {
+    if (nt == 1) { /* small tables: the same read-only pass on the calling thread */
+        jobs[0] = (Job){devs, 0, nd, nd, Q, hQ, fq, f64, i64, cls, cls + nd, &bail};
+        worker(&jobs[0]);
+    }
+    for (int t = 0; t < nt && nt > 1; ++t) {
         jobs[t] = (Job){devs, nd * t / nt, nd * (t + 1) / nt, nd, Q, hQ, fq, f64, i64, cls, cls + nd, &bail};
         if (pthread_create(&th[t], NULL, worker, &jobs[t]) != 0) { bail = 1; break; }
         ++started;
@@ -596,6 +601,38 @@ fail:
     return NULL;
 }
 
+/* sets(os_class) -> {"M1": [...], "M2": [...], "M3": [...]}: the device indices of class 1 / 2 / 3 of
+ * one fleet's class row, in device order (assign_sets, dense_common.py:149-167) */
+static PyObject *sets_of(PyObject *self, PyObject *args) {
+    (void)self;
+    Py_buffer bc;
+    if (!PyArg_ParseTuple(args, "y*", &bc)) return NULL;
+    const uint8_t *cl = (const uint8_t *)bc.buf;
+    const Py_ssize_t M = bc.len;
+    PyObject *sets = PyDict_New(), *v = NULL;
+    if (!sets) goto fail;
+    for (int s = 1; s <= 3; ++s) {
+        Py_ssize_t cnt = 0;
+        for (Py_ssize_t i = 0; i < M; ++i) cnt += cl[i] == s;
+        if (!(v = PyList_New(cnt))) goto fail;
+        for (Py_ssize_t i = 0, j = 0; i < M; ++i)
+            if (cl[i] == s) {
+                PyObject *ix = PyLong_FromSsize_t(i);
+                if (!ix) goto fail;
+                PyList_SET_ITEM(v, j++, ix);
+            }
+        if (PyDict_SetItem(sets, s_m[s - 1], v)) goto fail;
+        Py_CLEAR(v);
+    }
+    PyBuffer_Release(&bc);
+    return sets;
+fail:
+    Py_XDECREF(sets);
+    Py_XDECREF(v);
+    PyBuffer_Release(&bc);
+    return NULL;
+}
+
 static PyObject *results(PyObject *self, PyObject *args) {
     (void)self;
     PyObject *cls;
@@ -641,6 +678,7 @@ done:
 static PyMethodDef methods[] = {{"pack", pack, METH_VARARGS, "Pack fleets of DeviceProfile into the fleet table."},
                                 {"consts", consts, METH_VARARGS, "Per-fleet obj_value constants of a packed table."},
                                 {"results", results, METH_VARARGS, "HALDAResult per fleet of a solved batch."},
+                                {"sets", sets_of, METH_VARARGS, "M1 / M2 / M3 device index lists of a class row."},
                                 {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_fleetpack", NULL, -1, methods, NULL, NULL, NULL, NULL};

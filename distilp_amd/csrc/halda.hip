@@ -715,6 +715,11 @@ int halda_debug_stamps(unsigned long long *out, int n_inst) {
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halda_stamps), sizeof(unsigned long long) * kStamps * n));
     return n;
 }
+int halda_debug_dump(double *out) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halda_dump), sizeof(double) * kDumpFleets * kDumpDev * kDumpE * 2));
+    return kDumpFleets;
+}
 #endif
 
 int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,

@@ -20,6 +20,9 @@ enum { CLS_DONE = 0, CLS_K1 = 1, CLS_GEN = 2, CLS_GEN1 = 3, CLS_BIG = 4 };
 #ifdef HALDA_STAMPS
 constexpr int kStampInst = 65536, kStamps = 12;
 __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
+// the k = 2 tables G / H of the k-slot kernel's fleets (tools/kslot_tables.py): [fleet][device][e]
+constexpr int kDumpFleets = 4096, kDumpDev = 16, kDumpE = 32;
+__device__ double g_halda_dump[kDumpFleets * kDumpDev * kDumpE * 2];
 #define HALDA_STAMP(k)                                                                                  \
     do {                                                                                                \
         if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -237,6 +240,41 @@ __device__ inline T row16_reduce(T v, Op op) {
     v = op(v, ror16<2>(v));
     v = op(v, ror16<1>(v));
     return v;
+}
+
+// Arg-reductions over a 16-lane row by the same rotations, on (key, lane index) pairs compared
+// lexicographically -- the min with the LOWEST index among equal keys, the max with the HIGHEST --
+// carrying one payload value of the winning lane: every lane of the row ends with the row's extreme
+// key, the index the ballot-based lowest() / highest() would give and that lane's payload, with no
+// LDS round trip (a bpermute) in the chain. The order is total, so the result is that of any order.
+template <int R>
+__device__ inline void argmin16_step(double &k, int &i, double &p) {
+    const double k2 = ror16<R>(k), p2 = ror16<R>(p);
+    const int i2 = ror16<R>(i);
+    const bool t = (k2 < k) | ((k2 == k) & (i2 < i));
+    k = t ? k2 : k;
+    i = t ? i2 : i;
+    p = t ? p2 : p;
+}
+__device__ inline void argmin16(double &k, int &i, double &p) {
+    argmin16_step<8>(k, i, p);
+    argmin16_step<4>(k, i, p);
+    argmin16_step<2>(k, i, p);
+    argmin16_step<1>(k, i, p);
+}
+template <int R>
+__device__ inline void argmax16_step(double &k, int &i) {
+    const double k2 = ror16<R>(k);
+    const int i2 = ror16<R>(i);
+    const bool t = (k2 > k) | ((k2 == k) & (i2 > i));
+    k = t ? k2 : k;
+    i = t ? i2 : i;
+}
+__device__ inline void argmax16(double &k, int &i) {
+    argmax16_step<8>(k, i);
+    argmax16_step<4>(k, i);
+    argmax16_step<2>(k, i);
+    argmax16_step<1>(k, i);
 }
 
 // Lanes per problem: Seg<64> = the whole wave (reductions, ballots and broadcasts as above);

@@ -1618,6 +1618,18 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     const int nf = A.F.n_fleets;
     const int64_t f = int64_t(blockIdx.x) * kPer + seg;
     SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
+    {
+        // the slot with the largest k > 1 tables (C2: k = 2) is the workgroup's critical path: its
+        // threshold scan is the last thing running. It gets the SIMD's issue priority over the other
+        // slots' waves (of other workgroups) it shares the SIMD with.
+        int crit = -1, r1 = 0;
+        for (int p = 0; p < SA.n_slot; ++p)
+            if (SA.tab[p] > 0 && SA.r1[p] > r1) {
+                r1 = SA.r1[p];
+                crit = p;
+            }
+        if (q == crit) __builtin_amdgcn_s_setprio(3);
+    }
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
     // XCC_ID[3:0] above
@@ -1633,6 +1645,16 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         __syncthreads();  // every slot's tables are complete
         HALDA_KSTAMPW(11, __builtin_amdgcn_s_memtime());
         const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
+#ifdef HALDA_STAMPS
+        if (f < kDumpFleets && A.ks[SA.j[q]] == 2 && SA.tab[q] > 0 && lane % kSegLanes < fd.M) {
+            const int R1 = A.Ws[SA.j[q]] - fd.M + 1, RS = odd_stride(R1), i = lane % kSegLanes;
+            for (int e = 0; e < kDumpE; ++e) {
+                const int64_t o = ((int64_t(f) * kDumpDev + i) * kDumpE + e) * 2;
+                g_halda_dump[o] = e < R1 ? w.G[i * RS + e] : kInf;
+                g_halda_dump[o + 1] = e < R1 ? w.H[i * RS + e] : kInf;
+            }
+        }
+#endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
         if (f < nf) sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec);
         HALDA_KSTAMPW(7, t_rec[2]);

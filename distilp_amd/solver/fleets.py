@@ -25,6 +25,7 @@ s_disk the objective constant divides by).
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass, replace
 from typing import Iterable, List, Optional, Sequence
 
@@ -98,15 +99,11 @@ def _bind(lib):
 
 
 def model_struct(model: ModelProfile, kv_factor: float) -> HaldaModelC:
-    m = HaldaModelC()
-    m.has_f_q = int("b_1" in model.f_q)
-    m.f_q_b1 = float(model.f_q["b_1"]) if m.has_f_q else 0.0
-    m.has_f_out = int("b_1" in model.f_out)
-    m.f_out_b1 = float(model.f_out["b_1"]) if m.has_f_out else 0.0
-    m.b_prime = float(b_prime(model, kv_bits_k=kv_factor))
-    m.b_layer, m.b_in, m.b_out, m.V = float(model.b_layer), float(model.b_in), float(model.b_out), float(model.V)
-    m.L = int(model.L)
-    return m
+    fq, fo = model.f_q, model.f_out
+    has_q, has_o = "b_1" in fq, "b_1" in fo
+    return HaldaModelC(float(fq["b_1"]) if has_q else 0.0, float(fo["b_1"]) if has_o else 0.0, int(has_q),
+                       int(has_o), float(b_prime(model, kv_bits_k=kv_factor)), float(model.b_layer),
+                       float(model.b_in), float(model.b_out), float(model.V), int(model.L))
 
 
 @dataclass
@@ -472,6 +469,80 @@ class MultiDeviceContext:
     def solve(self, table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
               want_x: bool = False) -> "FleetSolve":
         return solve_table(table, model, ks, kv_factor, want_x=want_x, _multi=self)
+
+
+class _OneFleet:
+    """Per-thread workspace of the single-fleet path (`solve_one`, i.e. every `halda_solve`): the
+    packer's blocks, the C structs pointing at them and the result buffers for one (devices,
+    k-candidates) shape, reused while the shape repeats -- no per-call allocation or struct filling.
+    The results are overwritten by the thread's next call: callers copy what they keep."""
+
+    def __init__(self, nd: int, ks: Sequence[int]):
+        nk = len(ks)
+        self.nd, self.ks = nd, list(ks)
+        self.karr = np.asarray(self.ks, np.int32)
+        self.f64 = np.empty((len(F64_FIELDS), nd))
+        self.i64 = np.empty((len(I64_FIELDS), nd), np.int64)
+        self.u8 = np.empty((2, nd), np.uint8)
+        self.off = np.empty(2, np.int64)
+        self.heads = np.empty(1, np.int64)
+        self.consts = np.empty(3)
+        # halda_fleets: {int32 n_fleets, min_devices, max_devices; 19 pointers} = 21 u64 slots
+        self.hdr = np.zeros(21, np.uint64)
+        pu, pf, pi = self.u8.ctypes.data, self.f64.ctypes.data, self.i64.ctypes.data
+        self.hdr[0] = 1 | (nd << 32)
+        self.hdr[1] = nd
+        self.hdr[2:5] = [self.off.ctypes.data, pu, pu + nd]
+        self.hdr[5:15] = pf + 8 * nd * np.arange(len(F64_FIELDS), dtype=np.uint64)
+        self.hdr[15:21] = pi + 8 * nd * np.arange(len(I64_FIELDS), dtype=np.uint64)
+        self.fs = HaldaFleetsC.from_buffer(self.hdr)
+        xs = 7 * nd + 1
+        self.fbuf = np.zeros(1 + nk + 2 * nk * xs)
+        self.ibuf = np.zeros(1 + 2 * nd + nk, np.int32)
+        pF, pI = self.fbuf.ctypes.data, self.ibuf.ctypes.data
+        o2 = 1 + nk
+        self.status = self.ibuf[1 + 2 * nd:]
+        self.x = self.fbuf[o2:o2 + nk * xs].reshape(nk, xs)
+        self.c = self.fbuf[o2 + nk * xs:].reshape(nk, xs)
+        self.res = HaldaFleetResultC(pI, pF, pI + 4, pI + 4 * (1 + nd), pF + 8, pI + 4 * (1 + 2 * nd), pF + 8 * o2,
+                                     pF + 8 * (o2 + nk * xs), None)
+
+
+_TLS = threading.local()
+
+
+def pack_one(devs: Sequence[DeviceProfile], model: ModelProfile, ks: Sequence[int]) -> "_OneFleet":
+    """One fleet (the `halda_solve` path) packed by the C packer into the thread's workspace for the
+    k-candidates `ks` (ascending, > 0); raises the reference's coefficient / kappa exceptions as
+    fleet_table does. ws.u8[0] holds the device classes."""
+    if _PACKER is None or not hasattr(_PACKER, "sets"):
+        raise RuntimeError("pack_one needs the C packer (distilp_amd/csrc/fleetpack.c)")
+    nd = len(devs)
+    ws = getattr(_TLS, "one", None)
+    if ws is None or ws.nd != nd or ws.ks != ks:
+        ws = _TLS.one = _OneFleet(nd, ks)
+    _PACKER.pack([devs], model.Q, "b_1" in model.f_q, "b_1" in model.f_out, ws.f64, ws.i64, ws.u8, ws.off, ws.heads)
+    return ws
+
+
+def sweep_one(ws: "_OneFleet", model: ModelProfile, kv_factor: float, device: int = 0) -> "_OneFleet":
+    """The packed fleet of `ws` swept over its k-candidates by halda_solve_fleets_host, x and c of every
+    k returned (ws.status [n_k], ws.x / ws.c [n_k, 7 M + 1]), and its obj_value constants (sum t_comm,
+    sum xi, kappa in the reference's order, the packer's C loops) in ws.consts. The thread's next call
+    overwrites them."""
+    ctx = get_context(device)
+    lib = _bind(ctx.lib)
+    m = model_struct(model, kv_factor)
+    with ctx._lock:
+        rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(ws.fs), ws.karr.ctypes.data,
+                                         len(ws.ks), ctypes.byref(ws.res))
+    if rc != 0:
+        raise RuntimeError(f"halda_solve_fleets_host failed ({rc}): {last_error(lib)}")
+    fo = model.f_out
+    has_o = "b_1" in fo
+    _PACKER.consts(ws.f64, ws.i64, ws.u8, ws.off, ws.heads, has_o, float(fo["b_1"]) if has_o else 0.0,
+                   float(model.b_in), float(model.b_out), float(model.V), ws.consts)
+    return ws
 
 
 def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,

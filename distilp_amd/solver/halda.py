@@ -32,7 +32,7 @@ import numpy as np
 from ..common import DeviceProfile, ModelProfile
 from ._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL
 from .coefficients import HALDAResult, ILPResult, assign_sets, kappa_constant, valid_factors_of_L
-from .fleets import _PACKER, fleet_constants, fleet_table, solve_table
+from .fleets import _PACKER, fleet_constants, fleet_table, pack_one, solve_table, sweep_one
 from .lower import kv_bits_to_factor
 
 
@@ -53,23 +53,43 @@ def _offset_parts(devs, model: ModelProfile, sets) -> Tuple[float, float, float]
     return t_comm, xi_sum, kappa
 
 
+def _construct(cls, **fields):
+    """cls.model_construct(**fields) for a model whose fields are all given, already typed: the field
+    dict, its own fields-set, no extra / private state (what model_construct sets), without its
+    per-call field walk."""
+    o = _new(cls)
+    _setattr(o, "__dict__", fields)
+    _setattr(o, "__pydantic_fields_set__", set(fields))
+    _setattr(o, "__pydantic_extra__", None)
+    _setattr(o, "__pydantic_private__", None)
+    return o
+
+
+_new, _setattr = object.__new__, object.__setattr__
+
+
 def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: float, device: int,
-                  debug: bool) -> List[Tuple[int, Optional[ILPResult]]]:
+                  debug: bool, _cls_out: Optional[list] = None) -> List[Tuple[int, Optional[ILPResult]]]:
     """Every k of one fleet lowered, solved and returned by ONE halda_solve_fleets call (the CSR is
     built on the GPU, bit-identical to lower.lower_fleet); obj_value = c.x + offsets formed here with
     NumPy on the returned c and x, exactly as the reference forms it (halda_p_solver.py:347-357).
 
     Errors surface where the reference's k loop (halda_p_solver.py:391-412) raises them: k = 0 at
     W = L // k (:72), then the k-independent coefficient errors (b_1 missing, zero T_cpu / s_disk,
-    empty fleet) at the first k, after that k's debug line."""
+    empty fleet) at the first k, after that k's debug line. `sets` is not read (the reference's sets
+    come from the same device classes the packer writes); _cls_out, when given, receives a copy of the
+    packed device classes (halda_solve builds the result's sets from them)."""
+    pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
+    # the C packer's single-fleet workspace (no per-call allocation), else a FleetTable
+    one = bool(pos) and _PACKER is not None and hasattr(_PACKER, "sets")
     try:
-        table = fleet_table([devs], model)  # the reference's coefficient / kappa errors, raised by the packer
+        ws = pack_one(devs, model, pos) if one else fleet_table([devs], model)  # the reference's errors
         err = None
     except Exception as e:  # noqa: BLE001 -- re-raised at the first k, as the reference raises it
         err = e
-    pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
     M, N = len(devs), 7 * len(devs) + 1
-    res = None
+    swept = False
+    status = X = C = None
     out: List[Tuple[int, Optional[ILPResult]]] = []
     for k in Ks:
         if debug:
@@ -80,19 +100,29 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
             raise err
         r: Optional[ILPResult] = None
         if k > 0:
-            if res is None:
-                res = solve_table(table, model, pos, kv_factor, device, want_x=True)
-                # sum t_comm, sum xi, kappa in the reference's order (the packer's C loops)
-                offsets = tuple(float(v[0]) for v in fleet_constants(table, model))
+            if not swept:
+                swept = True
+                if one:
+                    sweep_one(ws, model, kv_factor, device)
+                    status, X, C = ws.status, ws.x, ws.c
+                    t_comm, xi_sum, kappa = (float(v) for v in ws.consts)
+                    cls_row = ws.u8[0]
+                else:
+                    res = solve_table(ws, model, pos, kv_factor, device, want_x=True)
+                    status, X, C = res.status[0], res.x[0], res.c[0]
+                    # sum t_comm, sum xi, kappa in the reference's order (the packer's C loops)
+                    t_comm, xi_sum, kappa = (float(v[0]) for v in fleet_constants(ws, model))
+                    cls_row = ws.os_class
+                if _cls_out is not None:
+                    _cls_out.append(np.array(cls_row, np.uint8))
             j = pos.index(k)
-            st = int(res.status[0, j])
+            st = int(status[j])
             if st == STATUS_OPTIMAL:
-                x = np.array(res.x[0, j, :N])
-                c = np.array(res.c[0, j, :N])
-                t_comm, xi_sum, kappa = offsets
+                x = np.array(X[j, :N])
+                c = np.array(C[j, :N])
                 obj = float(c.dot(x)) + t_comm + xi_sum + kappa
                 wn = np.rint(x[:2 * M]).astype(np.int64).tolist()  # int(round(v)): both round half to even
-                r = ILPResult.model_construct(k=k, w=wn[:M], n=wn[M:], obj_value=obj)  # fields already typed
+                r = _construct(ILPResult, k=k, w=wn[:M], n=wn[M:], obj_value=obj)  # fields already typed
             elif st != STATUS_INFEASIBLE:
                 raise RuntimeError(f"libhalda rejected the k={k} MILP with status {st}: "
                                    "the lowered MILP does not have the HALDA structure")
@@ -124,15 +154,16 @@ def halda_solve(
     Ks = _k_list(model, k_candidates)
     kv_factor = kv_bits_to_factor(kv_bits)
     devs = list(devs)
-    sets = assign_sets(devs)
     if debug:
         print("Objectives by k")
-    per_k = _sweep_on_gpu(devs, model, sets, Ks, kv_factor, device, debug) if Ks else []
+    cls: list = []
+    per_k = _sweep_on_gpu(devs, model, None, Ks, kv_factor, device, debug, cls) if Ks else []
     best = _pick(per_k)
     if best is None:
         raise RuntimeError("No feasible MILP found for any k this round.")
-    result = HALDAResult.model_construct(w=list(best.w), n=list(best.n), k=best.k, obj_value=best.obj_value,
-                                         sets={k: list(v) for k, v in sets.items()})
+    # the device sets (dense_common.py:149-167) from the classes the packer wrote
+    sets = _PACKER.sets(cls[0]) if cls and _PACKER is not None and hasattr(_PACKER, "sets") else assign_sets(devs)
+    result = _construct(HALDAResult, w=list(best.w), n=list(best.n), k=best.k, obj_value=best.obj_value, sets=sets)
     if plot:
         from .plotter import plot_k_curve
 
