@@ -85,8 +85,22 @@ struct Ctx {
     bool last_fleet_fused = false;
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
     size_t shard_bytes = 0;
-    void *fflag = nullptr;         // per-fleet "needs the table launch" bytes of the fused sweep
-    size_t fflag_bytes = 0;
+    // The fused sweep's scratch (per-fleet "needs the table launch" bytes, the hand-back flag) per
+    // stream: launches on one stream are ordered by it, so batches enqueued on different streams use
+    // different slots and need no cross-stream ordering (they overlap on the device). A slot moving to
+    // another stream waits for the launches already enqueued on the stream it leaves.
+    struct SweepSlot {
+        hipStream_t stream = nullptr;
+        bool used = false;
+        uint64_t tick = 0;
+        uint8_t *fflag = nullptr;
+        size_t fflag_bytes = 0;
+        int *hb = nullptr;
+        hipEvent_t ev = nullptr;
+    };
+    static constexpr int kSweepSlots = 8;
+    SweepSlot sws[kSweepSlots];
+    uint64_t sws_tick = 0;
     hipStream_t last_stream = nullptr;
     bool have_last = false;
     void *fleet_scratch = nullptr;  // lowered batch + results of halda_solve_fleets
@@ -170,6 +184,38 @@ int order_after_previous(Ctx *ctx, hipStream_t s) {
     }
     ctx->last_stream = s;
     ctx->have_last = true;
+    return HALDA_OK;
+}
+
+// The fused sweep's scratch slot for stream s with room for nf fleet flags (see Ctx::SweepSlot).
+int sweep_slot(Ctx *c, hipStream_t s, int64_t nf, Ctx::SweepSlot **out) {
+    Ctx::SweepSlot *slot = nullptr;
+    for (auto &x : c->sws)
+        if (x.used && x.stream == s) slot = &x;
+    if (!slot) {
+        for (auto &x : c->sws)
+            if (!slot || (!x.used && slot->used) || (x.used == slot->used && x.tick < slot->tick)) slot = &x;
+        if (slot->used) {  // taken over from another stream: after everything enqueued there so far
+            HIP_TRY(hipEventRecord(slot->ev, slot->stream));
+            HIP_TRY(hipStreamWaitEvent(s, slot->ev, 0));
+        } else {
+            HIP_TRY(hipEventCreateWithFlags(&slot->ev, hipEventDisableTiming));
+            HIP_TRY(hipMalloc(&slot->hb, 256));
+            HIP_TRY(hipMemsetAsync(slot->hb, 0, 256, s));
+            slot->used = true;
+        }
+        slot->stream = s;
+    }
+    slot->tick = ++c->sws_tick;
+    const size_t need = (size_t(nf) + 255) & ~size_t(255);
+    if (need > slot->fflag_bytes) {
+        if (slot->fflag) HIP_TRY(hipFree(slot->fflag));  // hipFree waits for the device
+        slot->fflag = nullptr;
+        slot->fflag_bytes = 0;
+        HIP_TRY(hipMalloc(&slot->fflag, need));
+        slot->fflag_bytes = need;
+    }
+    *out = slot;
     return HALDA_OK;
 }
 
@@ -343,19 +389,11 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
     // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
     const bool gate = tables_first || r1_k1 > kDpLanes;
-    const bool scratch = !(reg_mode && !gate);  // flags / hand-back flag of this context in use
+    const bool scratch = !(reg_mode && !gate);  // flags / hand-back flag of this stream's slot in use
+    Ctx::SweepSlot *slot = nullptr;
     if (scratch) {
-        const int rc = order_after_previous(c, s);
+        const int rc = sweep_slot(c, s, nf, &slot);
         if (rc != HALDA_OK) return rc;
-    }
-    // staging: ks and the per-fleet flags
-    const size_t need = 256 + ((size_t(nf) + 255) & ~size_t(255));
-    if (need > c->fflag_bytes) {
-        if (c->fflag) HIP_TRY(hipFree(c->fflag));
-        c->fflag = nullptr;
-        c->fflag_bytes = 0;
-        HIP_TRY(hipMalloc(&c->fflag, need));
-        c->fflag_bytes = need;
     }
     SweepArgs A = {};
     A.Mo = model;
@@ -370,8 +408,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
              (c->x_zero ? kOutXZ : 0);
     A.x_off = out.x_off;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
-    A.fflag = scratch ? static_cast<uint8_t *>(c->fflag) + 256 : nullptr;
-    A.hb_flag = c->hb_flag;
+    A.fflag = scratch ? slot->fflag : nullptr;
+    A.hb_flag = scratch ? slot->hb : c->hb_flag;
     A.launch_id = ++c->launch_id;
     A.mmax = mmax;
     A.uM = F.min_devices == F.max_devices ? F.max_devices : 0;
@@ -593,7 +631,11 @@ void halda_free(void *ctx) {
     if (c->hb_flag) (void)hipFree(c->hb_flag);
     if (c->fleet_scratch) (void)hipFree(c->fleet_scratch);
     if (c->gtab) (void)hipFree(c->gtab);
-    if (c->fflag) (void)hipFree(c->fflag);
+    for (auto &x : c->sws) {
+        if (x.fflag) (void)hipFree(x.fflag);
+        if (x.hb) (void)hipFree(x.hb);
+        if (x.ev) (void)hipEventDestroy(x.ev);
+    }
     if (c->shard) (void)hipFree(c->shard);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_host) (void)hipEventDestroy(c->ev_host);

@@ -242,41 +242,6 @@ __device__ inline T row16_reduce(T v, Op op) {
     return v;
 }
 
-// Arg-reductions over a 16-lane row by the same rotations, on (key, lane index) pairs compared
-// lexicographically -- the min with the LOWEST index among equal keys, the max with the HIGHEST --
-// carrying one payload value of the winning lane: every lane of the row ends with the row's extreme
-// key, the index the ballot-based lowest() / highest() would give and that lane's payload, with no
-// LDS round trip (a bpermute) in the chain. The order is total, so the result is that of any order.
-template <int R>
-__device__ inline void argmin16_step(double &k, int &i, double &p) {
-    const double k2 = ror16<R>(k), p2 = ror16<R>(p);
-    const int i2 = ror16<R>(i);
-    const bool t = (k2 < k) | ((k2 == k) & (i2 < i));
-    k = t ? k2 : k;
-    i = t ? i2 : i;
-    p = t ? p2 : p;
-}
-__device__ inline void argmin16(double &k, int &i, double &p) {
-    argmin16_step<8>(k, i, p);
-    argmin16_step<4>(k, i, p);
-    argmin16_step<2>(k, i, p);
-    argmin16_step<1>(k, i, p);
-}
-template <int R>
-__device__ inline void argmax16_step(double &k, int &i) {
-    const double k2 = ror16<R>(k);
-    const int i2 = ror16<R>(i);
-    const bool t = (k2 > k) | ((k2 == k) & (i2 > i));
-    k = t ? k2 : k;
-    i = t ? i2 : i;
-}
-__device__ inline void argmax16(double &k, int &i) {
-    argmax16_step<8>(k, i);
-    argmax16_step<4>(k, i);
-    argmax16_step<2>(k, i);
-    argmax16_step<1>(k, i);
-}
-
 // Lanes per problem: Seg<64> = the whole wave (reductions, ballots and broadcasts as above);
 // Seg<16> = four problems per wave, each on a 16-lane DPP row (row rotations for the reductions,
 // ballots shifted to the row, broadcasts are bpermutes from the row). Sums over a 16-device problem

@@ -229,6 +229,38 @@ def test_register_launches_overlap_on_two_streams(llama_online_model):
         assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)
 
 
+@pytest.mark.parametrize("n_streams", [3, 10])
+def test_table_launches_on_many_streams(llama_online_model, n_streams):
+    """Launches that use the fused sweep's scratch (per-fleet flags, hand-back flag: the k-slot launch
+    of C2-shaped batches and its gated table launch) take a scratch slot per stream, so batches on
+    different streams need no ordering between them; more streams than slots hand a slot over after
+    the launches of the stream it leaves. Batches of 16- and 10-device fleets (every k of L = 80)
+    alternating over the streams give the results of one synchronous call each, per-k outputs
+    included."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    shapes = [16, 10, 16]
+    tables = [fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)]
+                           for s in range(b * 130, b * 130 + 130)], llama_online_model) for b, M in enumerate(shapes)]
+    want = [solve_table(t, llama_online_model, ks, 0.5) for t in tables]
+    dts = [DeviceFleetTable(t, llama_online_model, ks, 0.5, dev, want_per_k=True) for t in tables]
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+    for i in range(3 * n_streams):
+        dts[i % len(dts)].launch(ctx, streams[i % n_streams].cuda_stream)
+    torch.cuda.synchronize(dev)
+    for d, w in zip(dts, want):
+        assert np.array_equal(d.out["best_k"].cpu().numpy(), w.best_k)
+        assert np.array_equal(d.out["w"].cpu().numpy(), w.w) and np.array_equal(d.out["n"].cpu().numpy(), w.n)
+        assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)
+        assert np.array_equal(d.out["status"].cpu().numpy(), w.status.ravel())
+        assert np.array_equal(d.out["obj_by_k"].cpu().numpy(), w.obj_by_k.ravel())
+
+
 @pytest.mark.parametrize("M", [64, 12])
 def test_uniform_fleets_viewed_from_an_offset_dev_off(llama_online_model, M):
     """A device-resident table viewed from fleet 7 on (dev_off pointing into the middle, so dev_off[0]
