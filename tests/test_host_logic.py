@@ -354,3 +354,35 @@ def test_batch_results_c_builder_equals_python(llama_online_model, monkeypatch, 
     live = [g for g in got if g is not None]
     live[0].k = 99
     assert live[1].k != 99 and "k" in live[1].model_fields_set
+
+
+def test_bench_gpus_n_spawns_one_rank_per_gpu(monkeypatch):
+    """`python bench.py --gpus 8` (no WORLD_SIZE yet) starts its ranks itself before touching the GPU:
+    torch.distributed.run with one process per GPU on 127.0.0.1, the same bench arguments (RCCL
+    backend by default), and relays the launcher's exit code."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo))
+    import bench
+
+    seen = {}
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return subprocess.CompletedProcess(cmd, 3)
+
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5"])
+    assert bench.main() == 3
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
+    assert "--backend" not in cmd  # nccl (RCCL) is the default backend of the ranks
