@@ -280,6 +280,7 @@ __device__ inline bool split_full(const Dev &d, int w, double &g, int &n, int s[
 }
 
 __device__ inline bool split_first(const Dev &d, int w, double &g, int &n, int s[4]) { return split_full(d, w, g, n, s); }
+__device__ inline bool split_second(const Dev &d, int w, double &g, int &n, int s[4]) { return split_full(d, w, g, n, s); }
 
 // Incremental step w-1 -> w. The cost is L-natural convex in (w, n) (every term
 // depends on w, n or w - n only; validated at decode), so the least minimiser
@@ -1468,7 +1469,7 @@ __device__ int k1_alloc(const Rec &rec, int M, int R, const SG &sg, int &e, int 
         double ga, gb;
         int na, nb, sb[4];
         const bool fa = split_first(d, wlo, ga, na, s);
-        const bool fb = split_full(d, wlo + 1, gb, nb, sb);
+        const bool fb = split_second(d, wlo + 1, gb, nb, sb);
         ok0 = wlo <= whi && fa;
         ok1 = ok0 && wlo + 1 <= whi && fb;
         g0 = ok0 ? ga : g0;

@@ -564,6 +564,29 @@ __device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, 
     }
     return ok;
 }
+// split_full at w = 2 (the greedy's first increment): 0 <= nL <= n <= nU <= 2, so the three tries
+// n = 0, 1, 2 (clamped to [nL, nU]) cover every candidate split_full tries (its kinks clamp into the
+// same range) with the same cost expression and tie rule: the same minimum and least minimiser, one
+// try fewer than split_full's four.
+__device__ inline bool split_second(const FieldRec &r, int w, double &g, int &n, int s[4]) {
+    if (w != 2) return split_full(r, w, g, n, s);
+    int nL, nU;
+    const bool okI = rec_interval(r, w, nL, nU);
+    const double pv = rec_pv(r), aw = r.alpha * double(w);
+    const bool own = rec_own(r);
+    double best = kInf;
+    int bn = -1;
+    rec_try(r, aw, pv, own, w, 0, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, 1, nL, nU, best, bn);
+    rec_try(r, aw, pv, own, w, 2, nL, nU, best, bn);
+    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
+    if (ok) {
+        g = best;
+        n = bn;
+        rec_slacks(r, w, bn, s);
+    }
+    return ok;
+}
 __device__ inline bool split_full(const UFieldRec &r, int w, double &g, int &n, int s[4]) {
     return split_full_impl<true>(r, w, g, n, s);
 }
