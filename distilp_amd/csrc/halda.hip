@@ -95,6 +95,8 @@ struct Ctx {
         uint64_t tick = 0;
         uint8_t *fflag = nullptr;
         size_t fflag_bytes = 0;
+        uint8_t *cls = nullptr;  // the CSR pipeline's per-instance verdict bytes
+        size_t cls_bytes = 0;
         int *hb = nullptr;
         hipEvent_t ev = nullptr;
     };
@@ -187,6 +189,19 @@ int order_after_previous(Ctx *ctx, hipStream_t s) {
     return HALDA_OK;
 }
 
+// A stream's scratch slot (see Ctx::SweepSlot): grown to hold `need` bytes at *buf.
+int grow(uint8_t **buf, size_t *bytes, size_t need) {
+    need = (need + 255) & ~size_t(255);
+    if (need > *bytes) {
+        if (*buf) HIP_TRY(hipFree(*buf));  // hipFree waits for the device
+        *buf = nullptr;
+        *bytes = 0;
+        HIP_TRY(hipMalloc(buf, need));
+        *bytes = need;
+    }
+    return HALDA_OK;
+}
+
 // The fused sweep's scratch slot for stream s with room for nf fleet flags (see Ctx::SweepSlot).
 int sweep_slot(Ctx *c, hipStream_t s, int64_t nf, Ctx::SweepSlot **out) {
     Ctx::SweepSlot *slot = nullptr;
@@ -207,13 +222,9 @@ int sweep_slot(Ctx *c, hipStream_t s, int64_t nf, Ctx::SweepSlot **out) {
         slot->stream = s;
     }
     slot->tick = ++c->sws_tick;
-    const size_t need = (size_t(nf) + 255) & ~size_t(255);
-    if (need > slot->fflag_bytes) {
-        if (slot->fflag) HIP_TRY(hipFree(slot->fflag));  // hipFree waits for the device
-        slot->fflag = nullptr;
-        slot->fflag_bytes = 0;
-        HIP_TRY(hipMalloc(&slot->fflag, need));
-        slot->fflag_bytes = need;
+    if (nf > 0) {
+        const int rc = grow(&slot->fflag, &slot->fflag_bytes, size_t(nf));
+        if (rc != HALDA_OK) return rc;
     }
     *out = slot;
     return HALDA_OK;
@@ -234,12 +245,13 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     bool big = false;
     const GenShape ls = lds_shape(full, &big);
     const size_t n = size_t(in.n_inst);
-    if (n > ctx->work_bytes) {
-        if (ctx->work) HIP_TRY(hipFree(ctx->work));
-        ctx->work = nullptr;
-        ctx->work_bytes = 0;
-        HIP_TRY(hipMalloc(&ctx->work, (n + 255) & ~size_t(255)));
-        ctx->work_bytes = (n + 255) & ~size_t(255);
+    // the verdict bytes and the hand-back flag are this stream's (its scratch slot): launches on other
+    // streams need no ordering with this one; only the global tables of the big launch are shared
+    Ctx::SweepSlot *slot = nullptr;
+    {
+        int rc = sweep_slot(ctx, stream, 0, &slot);
+        if (rc == HALDA_OK) rc = grow(&slot->cls, &slot->cls_bytes, n);
+        if (rc != HALDA_OK) return rc;
     }
     // global tables of the big launch: one slice per resident wave, grown on demand
     int64_t gstride = 0;
@@ -259,11 +271,12 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
             ctx->gtab_bytes = need;
         }
     }
-    {
+    if (big) {
         const int rc = order_after_previous(ctx, stream);
         if (rc != HALDA_OK) return rc;
     }
-    uint8_t *cls = static_cast<uint8_t *>(ctx->work);
+    uint8_t *cls = slot->cls;
+    int *hb_flag = slot->hb;
     const int launch_id = ++ctx->launch_id;  // tags this launch's k = 1 hand-backs (no reset needed)
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
@@ -272,7 +285,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_screen_k1_kernel), lds1, &per_cu));
         hipLaunchKernelGGL(halda_screen_k1_kernel, dim3(unsigned(in.n_inst)), dim3(64), size_t(lds1), stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc), ctx->hb_flag, launch_id, int(ctx->xcd_swizzle));
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc), hb_flag, launch_id, int(ctx->xcd_swizzle));
         HIP_TRY(hipGetLastError());
         if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
     } else {
@@ -286,7 +299,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_kernel), lds1, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
         hipLaunchKernelGGL(halda_solve_k1_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls, mmax,
-                           ctx->hb_flag, launch_id);
+                           hb_flag, launch_id);
         HIP_TRY(hipGetLastError());
     }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evs, stream));
@@ -303,7 +316,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_kc, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
         hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_kc), stream, in, out, cls, ls.mmax,
-                           ls.r1, 0, ls.tab_kc, static_cast<const int *>(ctx->hb_flag), launch_id, 0, int(CLS_GEN));
+                           ls.r1, 0, ls.tab_kc, static_cast<const int *>(hb_flag), launch_id, 0, int(CLS_GEN));
         HIP_TRY(hipGetLastError());
     }
     {
@@ -313,7 +326,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         const int64_t cap = wide ? int64_t(ctx->cus) * per_cu : int64_t(ctx->cus);
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(cap, in.n_inst)));
         hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_k1), stream, in, out, cls, ls.mmax,
-                           ls.r1, ls.tab, 0, static_cast<const int *>(ctx->hb_flag), launch_id, int(!wide),
+                           ls.r1, ls.tab, 0, static_cast<const int *>(hb_flag), launch_id, int(!wide),
                            int(CLS_GEN1));
         HIP_TRY(hipGetLastError());
     }
@@ -633,6 +646,7 @@ void halda_free(void *ctx) {
     if (c->gtab) (void)hipFree(c->gtab);
     for (auto &x : c->sws) {
         if (x.fflag) (void)hipFree(x.fflag);
+        if (x.cls) (void)hipFree(x.cls);
         if (x.hb) (void)hipFree(x.hb);
         if (x.ev) (void)hipEventDestroy(x.ev);
     }

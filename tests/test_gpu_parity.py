@@ -318,3 +318,52 @@ def test_w_upper_bounds_are_honoured(llama_online_model, M, seed, case):
         assert lo <= x[0] <= hi and lo <= x[M // 2] <= hi
         if mo.uniqueness_margin_ok(b1, b2):
             assert np.array_equal(x[:2 * M], xo[:2 * M])
+
+
+@pytest.mark.parametrize("n_streams", [2, 9])
+def test_csr_batches_on_several_streams(llama_online_model, n_streams):
+    """The milp() replacement (halda_solve_batch_device) with its verdict bytes and hand-back flag in
+    the stream's scratch slot: batches alternating over 2 and 9 streams (more streams than slots: a
+    slot is handed over after the launches of the stream it leaves), k > 1 instances included (16-
+    device fleets), give the results of one synchronous call each, bit for bit."""
+    import torch
+
+    from distilp_amd.common import DeviceProfile
+
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    batches = []
+    for b, M in enumerate([16, 64, 12]):
+        fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(900 + 40 * b + s, M)] for s in range(40)]
+        lowered = [lower_fleet(devs, llama_online_model, "4bit") for devs in fleets]
+        batch, _ = assemble(lowered, [ks] * len(lowered))
+        batches.append((batch, ctx.solve(batch)))
+    fields = ("n_cols", "n_rows", "csr_off", "col_off", "row_off", "row_ptr", "col_idx", "val", "c", "col_lb",
+              "col_ub", "row_lb", "row_ub", "integrality")
+    runs = []
+    for batch, _ in batches:
+        keep = {f: torch.from_numpy(np.ascontiguousarray(getattr(batch, f))).to(dev) for f in fields}
+        n = batch.n_inst
+        out = {"status": torch.empty(n, dtype=torch.int32, device=dev),
+               "x": torch.zeros(batch.total_cols, dtype=torch.float64, device=dev),
+               "obj_lin": torch.empty(n, dtype=torch.float64, device=dev),
+               "dual_bound": torch.empty(n, dtype=torch.float64, device=dev),
+               "gap": torch.empty(n, dtype=torch.float64, device=dev),
+               "nodes": torch.empty(n, dtype=torch.int64, device=dev)}
+        runs.append((keep, out))
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+    ctx.set_timing(False)
+    try:
+        for i in range(3 * n_streams):
+            j = i % len(batches)
+            keep, out = runs[j]
+            ctx.solve_device({f: t.data_ptr() for f, t in keep.items()}, batches[j][0],
+                             {f: t.data_ptr() for f, t in out.items()}, stream=streams[i % n_streams].cuda_stream)
+        torch.cuda.synchronize(dev)
+    finally:
+        ctx.set_timing(True)
+    for (batch, want), (_, out) in zip(batches, runs):
+        assert np.array_equal(out["status"].cpu().numpy(), want.status)
+        assert np.array_equal(out["x"].cpu().numpy(), want.x)
+        assert np.array_equal(out["obj_lin"].cpu().numpy(), want.obj_lin)
