@@ -25,7 +25,10 @@
  * caller. halda_solve_batch() takes HOST pointers, copies them to the device
  * and keeps nothing after it returns except grow-only scratch inside ctx.
  * halda_solve_batch_device() takes DEVICE pointers and is asynchronous on the
- * given HIP stream. Calls on one ctx must be serialised; use one ctx per GPU.
+ * given HIP stream. Calls on one ctx must be serialised (from the host); the
+ * work they enqueue on different streams runs concurrently (the per-launch
+ * scratch is per stream), so independent batches may alternate over streams to
+ * keep several in flight. Use one ctx per GPU.
  * Errors: functions return 0 on success and a negative code otherwise; the
  * message of the last failure on the calling thread is in halda_last_error().
  */
