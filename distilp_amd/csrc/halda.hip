@@ -24,6 +24,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "halda.h"
@@ -76,6 +77,7 @@ struct Ctx {
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
+    bool kslot_split = true;                     // k-slot launch: the helper wave splits the longest scan
     int sweep_waves = 0;                         // > 0: the register launch as the pipelined kernel, this many waves
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
@@ -391,6 +393,36 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     }
     SA.pick_off = int(kslot_lds);
     kslot_lds += int64_t(64 / kSegLanes) * SA.n_slot * int64_t(sizeof(SlotPick));
+    // the helper wave takes the upper half of the threshold scan of the slot with the largest tables
+    // (C2: k = 2, the workgroup's critical path)
+    // (C2: k = 2, the workgroup's critical path), first thing after the tables: the wave of the
+    // lightest other slot (no tables: k = 1 / W = M; else the smallest tables), an extra wave only
+    // when there is no other slot
+    SA.helper = -1;
+    SA.helper_wave = -1;
+    if (c->kslot_split) {
+        int r1 = 0;
+        for (int q = 0; q < SA.n_slot; ++q)
+            if (SA.tab[q] > 0 && SA.r1[q] > r1) {
+                r1 = SA.r1[q];
+                SA.helper = q;
+            }
+        int light = 1 << 30;
+        for (int q = 0; q < SA.n_slot && SA.helper >= 0; ++q) {
+            const int work = SA.tab[q] > 0 ? SA.r1[q] : 0;
+            if (q != SA.helper && work <= light) {  // ties: the later slot (larger k, less work)
+                light = work;
+                SA.helper_wave = q;
+            }
+        }
+        if (SA.helper >= 0 && SA.helper_wave < 0) {
+            if (SA.n_slot < kMaxSlots) SA.helper_wave = SA.n_slot;
+            else SA.helper = -1;
+        }
+    }
+    kslot_lds = align16(kslot_lds);
+    SA.split_off = int(kslot_lds);
+    if (SA.helper >= 0) kslot_lds += int64_t(64 / kSegLanes) * int64_t(sizeof(SplitArea));
     const bool kslot = c->seg_sweep && c->kslot_sweep && fits && mmax <= kSegLanes && tab_kc > 0 && kslot_all &&
                        SA.n_slot >= 1 && nf > kSweepSmallBatch && kslot_lds <= kLdsBudget;
     const bool seg = !kslot && c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
@@ -437,8 +469,8 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_kslot_kernel), kslot_lds, nullptr));
         const int64_t groups = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
         A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_kslot_kernel, dim3(unsigned(groups)), dim3(64 * SA.n_slot), size_t(kslot_lds), s,
-                           A, SA);
+        hipLaunchKernelGGL(halda_sweep_kslot_kernel, dim3(unsigned(groups)), dim3(64 * kslot_waves(SA)),
+                           size_t(kslot_lds), s, A, SA);
         HIP_TRY(hipGetLastError());
         if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;
@@ -620,6 +652,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->sweep_waves = sw ? std::atoi(sw) : 0;
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
+    const char *ks = std::getenv("HALDA_KSLOT_SPLIT");
+    c->kslot_split = !(ks && ks[0] == '0');
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||

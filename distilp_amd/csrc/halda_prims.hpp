@@ -49,11 +49,12 @@ __device__ double g_halda_dump[kDumpFleets * kDumpDev * kDumpE * 2];
 #define HALDA_TSTAMP(slot) do {} while (0)
 #endif
 // k-slot kernel: per (workgroup, slot) wave, slots 0..4 shader clock (start, records done, solved,
-// after the barrier, pick done), 5 the constant-rate clock at start
+// after the barrier, pick done), 5 the constant-rate clock at start (the helper wave stamps nothing)
 #define HALDA_KSTAMPW(slot, v)                                                                          \
     do {                                                                                                \
         const int64_t e_ = int64_t(blockIdx.x) * SA.n_slot + q;                                         \
-        if ((threadIdx.x & 63) == 0 && e_ < kStampInst) g_halda_stamps[e_ * kStamps + (slot)] = (v);    \
+        if (q < SA.n_slot && (threadIdx.x & 63) == 0 && e_ < kStampInst)                                \
+            g_halda_stamps[e_ * kStamps + (slot)] = (v);                                                \
     } while (0)
 #elif defined(HALDA_MARKS)  // asm listing only: phase markers for tools/asm_regions.py
 #define HALDA_SSTAMP(slot, v) asm volatile("; PHASE_MARK " #slot)

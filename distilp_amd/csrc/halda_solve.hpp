@@ -955,9 +955,38 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 // the pass-per-candidate scan: stop once (k-1) T + S(inf) >= best. Returns
 // false (caller runs the general scan) when a leaf is not convex / monotone.
 // On success st0 holds the allocation (table indices e_i).
+//
+// Split over two waves of a k-slot workgroup (16-lane segments only, sp != nullptr): the scan's
+// length is the workgroup's critical path, and each event is a dependent chain of reductions, so the
+// candidate range is cut at T_mid and both halves run at once. Part 1 (the slot's own wave) takes the
+// openings T <= T_mid; part 2 (the helper wave) starts from the optimal capped allocation at T_mid --
+// the state part 1 would reach there (the capped optimum is unique when no two devices tie on an
+// increment) -- and takes the rest, pruning with its own bound (never fewer events than the one scan
+// makes above T_mid). Part 1 then takes part 2's allocation when it is strictly better, so the
+// earliest T wins ties as in the one scan. T_mid = the lower median over the devices of H at
+// cap(T0) + 2 (tools/scan_model.py on dumped C2 tables: the longest scan 47 -> 28 events per wave).
+struct ScanSplit {
+    int part = 0;                // 0: no split, 1: openings T <= T_mid, 2: T > T_mid (the helper)
+    int *alt_e = nullptr;        // part 2's allocation (one int per segment lane), LDS
+    double *alt_best = nullptr;  // part 2's best objective, +inf when nothing beat its start, LDS
+    int *flag = nullptr;         // set by the helper once alt_e / alt_best are final, LDS
+};
+
+// Rank of v among the 16 lanes of its DPP row (ties: the lower lane first).
+template <int R>
+__device__ inline int rank_step(double v, int sl) {
+    const double u = ror16<R>(v);
+    const int j = (sl + R) & 15;
+    return (u < v || (u == v && j < sl)) ? 1 : 0;
+}
+template <int... R>
+__device__ inline int rank16(double v, int sl, std::integer_sequence<int, R...>) {
+    return (rank_step<R + 1>(v, sl) + ...);
+}
+
 template <class SG>
 __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &sg, double s_inf, double best0,
-                                    int64_t &nodes, const LeafInfo &li0) {
+                                    int64_t &nodes, const LeafInfo &li0, const ScanSplit sp = ScanSplit{}) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const double kc = I.kc;
     const int lane = sg.sl;  // device index within the problem
@@ -973,7 +1002,24 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     int cap = lo;
     if (act)
         while (cap < hi && H[cap + 1] <= T) ++cap;
-    // optimal capped allocation at T0 (greedy: every cap filled from lo, then the smallest increments)
+    double t_mid = kInf;  // part 1 stops past it, part 2 starts there
+    const int part = sp.part;
+    double t_stop = kInf;
+    if constexpr (SG::S == 16) {
+        if (part) {
+            const double v = act && cap < hi ? H[min(cap + 2, hi)] : kInf;
+            const int rank = rank16(v, lane, std::make_integer_sequence<int, 15>{});
+            const int n = sg.sum_i(v < kInf ? 1 : 0);
+            t_mid = sg.min_f64(v < kInf && rank == (n - 1) / 2 ? v : kInf);  // > T0; +inf: no opening at all
+            if (part == 1) t_stop = t_mid;
+            if (part == 2) {
+                T = t_mid;
+                if (act)
+                    while (cap < hi && H[cap + 1] <= T) ++cap;
+            }
+        }
+    }
+    // optimal capped allocation at T0 (part 2: at T_mid) (greedy: every cap filled from lo, then the smallest increments)
     int e = lo;
     int need = need_total;
     {
@@ -1016,15 +1062,16 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
         lam = sg.max_f64(lt);
         lj = sg.highest(lt == lam);
         if (kc * T + S < best) {
+            // part 2's start only bounds its pruning: part 1 already priced this allocation at a lower T
             best = kc * T + S;
-            bestE = e;
+            bestE = part == 2 ? -1 : e;
         }
     }
     while (true) {
         const bool useful = act && e == cap && cap < hi && (need > 0 || gn < lam);
         const double cand = useful ? hn : kInf;
         const double Tn = sg.min_f64(cand);
-        if (!(Tn < kInf) || !(kc * Tn + s_inf < best)) break;
+        if (!(Tn < kInf) || !(kc * Tn + s_inf < best) || Tn > t_stop) break;
         const int li = sg.lowest(cand == Tn);
         ++events;
         const double d = sg.bcast(gn, li);
@@ -1060,6 +1107,24 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     }
     nodes += events;
     HALDA_KSTAMP(5);
+    if constexpr (SG::S == 16) {
+        if (part == 2) {  // the helper: its result for part 1 (it posts the flag itself)
+            if (act && bestE >= 0) sp.alt_e[lane] = bestE;
+            if (lane == 0) *sp.alt_best = bestE >= 0 ? best : kInf;
+            wave_sync();
+            return true;
+        }
+        if (part == 1) {  // wait for the helper's half, keep the strictly better one
+            while (__hip_atomic_load(sp.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const double ab = *sp.alt_best;
+            if (ab < best) {
+                best = ab;
+                bestE = act ? sp.alt_e[lane] : 0;
+            }
+        }
+    }
     if (bestE >= 0) {  // a capped optimum beat the unconstrained allocation's own T
         if (act) w.st0[lane] = bestE;
     }
@@ -1074,7 +1139,7 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
 // Returns 1 solved (st0 = allocation), 0 infeasible, -1 not applicable (the table DP below runs).
 template <class SG>
 __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int64_t &nodes,
-                             unsigned long long *stamp = nullptr) {
+                             unsigned long long *stamp = nullptr, const ScanSplit sp = ScanSplit{}) {
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const int lane = sg.sl;
     const bool act = lane < M;
@@ -1151,7 +1216,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
 #ifdef HALDA_STAMPS
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();  // phase-0 greedy done
 #endif
-    kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li);
+    kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li, sp);
     wave_sync();
     return 1;
 }

@@ -1355,7 +1355,23 @@ struct SlotArgs {
     int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * (R + 1) + max_devices, 0: no tables
     int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
     int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
+    int helper;                // slot whose threshold scan is split over two waves (-1: none)
+    int helper_wave;           // the wave that takes its upper half first: a light slot's, or n_slot (extra)
+    int split_off;             // LDS byte offset of the split areas (SplitArea [4])
 };
+
+// What the helper wave hands to the split slot's wave, per segment (kc_scan_incremental, ScanSplit).
+struct SplitArea {
+    double alt_best;
+    int flag;
+    int pad;
+    int alt_e[kSegLanes];
+};
+
+// Waves of a k-slot workgroup: one per slot, plus the helper.
+__host__ __device__ inline int kslot_waves(const SlotArgs &SA) {
+    return SA.n_slot + (SA.helper >= 0 && SA.helper_wave == SA.n_slot ? 1 : 0);
+}
 
 // One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
 // its w / n candidate).
@@ -1405,7 +1421,7 @@ __device__ inline WaveCtx kslot_ctx(const SweepArgs &A, const SlotArgs &SA, int 
 }
 
 // Phase B of the k-slot workgroup: every wave builds an equal share of ALL the slots' k > 1 tables
-// (the (slot, entry) pairs in slot order, cut into n_slot contiguous stretches; lane = device; each
+// (the (slot, entry) pairs in slot order, cut into one contiguous stretch per wave; lane = device; each
 // stretch starts with a full split search, the same least minimisers as one chain, so the same
 // tables), instead of each k > 1 wave building its own while the W = M / k = 1 waves idle at the
 // barrier: the longest wave's dependent chain loses its table pass.
@@ -1414,7 +1430,8 @@ __device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, cons
     const int lane = sg.sl;
     int total = 0;
     for (int p = 0; p < SA.n_slot; ++p) total += SA.tab[p] > 0 ? SA.r1[p] : 0;
-    const int lo = q * total / SA.n_slot, hi = (q + 1) * total / SA.n_slot;
+    const int nw = kslot_waves(SA);
+    const int lo = q * total / nw, hi = (q + 1) * total / nw;
     int base = 0;
     for (int p = 0; p < SA.n_slot; ++p) {
         if (SA.tab[p] <= 0) continue;
@@ -1444,7 +1461,8 @@ __device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, cons
 }
 
 __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int j, int r1cap, int tabcap,
-                            const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec) {
+                            const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec,
+                            const ScanSplit sp) {
     using SG = Seg<kSegLanes>;
     constexpr int S = SG::S;
     const int lane = sg.sl;
@@ -1522,7 +1540,7 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
             } else {
                 // the tables were built by the whole workgroup (kslot_tables, before the barrier)
                 int64_t nodes = 0;
-                const int feas = dp_pass_lanes(w, I, sg, nodes, t_rec + 4);
+                const int feas = dp_pass_lanes(w, I, sg, nodes, t_rec + 4, sp);
 #ifdef HALDA_STAMPS
                 t_rec[2] = __builtin_amdgcn_s_memtime();
                 t_rec[3] = (unsigned long long)nodes;
@@ -1631,6 +1649,33 @@ __device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const 
     }
 }
 
+// The helper wave of a k-slot workgroup: the upper half (T > T_mid) of the split slot's threshold scan
+// for its segment's fleet -- the same leaf scan and phase-0 greedy as the slot's own wave, then
+// kc_scan_incremental part 2 into the split area -- and the flag, on every path (the slot's wave
+// waits for it only when its own scan ran to the end).
+__device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const KslotFleet &fd, SplitArea *ar,
+                             const Seg<kSegLanes> &sg, unsigned char *smem, int seg) {
+    const int p = SA.helper;
+    const int j = SA.j[p], k = A.ks[j], W = A.Ws[j];
+    if (sg.sl == 0) ar->alt_best = kInf;
+    if (kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) {
+        Inst I = {};
+        I.M = fd.M;
+        I.W = W;
+        I.Wd = double(W);
+        I.kc = double(k - 1);
+        I.iC = 7 * fd.M;
+        I.R1 = W - fd.M + 1;
+        I.RS = odd_stride(I.R1);
+        WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
+        w.st0 = ar->alt_e;  // the phase-0 allocation and part 2's result, not the slot's st0
+        int64_t nodes = 0;
+        (void)dp_pass_lanes(w, I, sg, nodes, nullptr, ScanSplit{2, ar->alt_e, &ar->alt_best, &ar->flag});
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (sg.sl == 0) __hip_atomic_store(&ar->flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int kPer = 64 / kSegLanes;
@@ -1651,8 +1696,9 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
                 r1 = SA.r1[p];
                 crit = p;
             }
-        if (q == crit) __builtin_amdgcn_s_setprio(3);
+        if (q == crit || (SA.helper >= 0 && q == SA.helper_wave)) __builtin_amdgcn_s_setprio(3);  // and its helper
     }
+    SplitArea *split = reinterpret_cast<SplitArea *>(smem + SA.split_off) + seg;
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
     // XCC_ID[3:0] above
@@ -1664,9 +1710,17 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         if (f < nf) fd = kslot_records(A, int(f), sg);
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
         if (f < nf) kslot_tables(A, SA, q, fd, sg, smem, seg);
+        if (SA.helper >= 0 && q == SA.helper_wave && sg.sl == 0) split->flag = 0;  // posted after the barrier
         HALDA_KSTAMPW(6, __builtin_amdgcn_s_memtime());
         __syncthreads();  // every slot's tables are complete
         HALDA_KSTAMPW(11, __builtin_amdgcn_s_memtime());
+        if (SA.helper >= 0 && q == SA.helper_wave) {  // the helper's half first: the split slot waits for it
+            if (f < nf) kslot_helper(A, SA, fd, split, sg, smem, seg);
+            if (q == SA.n_slot) {  // an extra wave: no slot of its own
+                __syncthreads();   // the pick barrier below
+                return;
+            }
+        }
         const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
 #ifdef HALDA_STAMPS
         if (f < kDumpFleets && A.ks[SA.j[q]] == 2 && SA.tab[q] > 0 && lane % kSegLanes < fd.M) {
@@ -1679,7 +1733,9 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         }
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
-        if (f < nf) sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec);
+        const ScanSplit sp{q == SA.helper ? 1 : 0, split->alt_e, &split->alt_best, &split->flag};
+        if (f < nf)
+            sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
         HALDA_KSTAMPW(7, t_rec[2]);
         HALDA_KSTAMPW(8, t_rec[3]);
         HALDA_KSTAMPW(9, t_rec[4]);
