@@ -77,7 +77,7 @@ struct Ctx {
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
-    bool kslot_split = true;                     // k-slot launch: the helper wave splits the longest scan
+    int kslot_split = 2;                         // k-slot launch: the longest scan split over this many waves
     int sweep_waves = 0;                         // > 0: the register launch as the pipelined kernel, this many waves
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
@@ -393,32 +393,42 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     }
     SA.pick_off = int(kslot_lds);
     kslot_lds += int64_t(64 / kSegLanes) * SA.n_slot * int64_t(sizeof(SlotPick));
-    // the helper wave takes the upper half of the threshold scan of the slot with the largest tables
-    // (C2: k = 2, the workgroup's critical path)
-    // (C2: k = 2, the workgroup's critical path), first thing after the tables: the wave of the
-    // lightest other slot (no tables: k = 1 / W = M; else the smallest tables), an extra wave only
-    // when there is no other slot
+    // the threshold scan of the slot with the largest tables (C2: k = 2, the workgroup's critical path)
+    // is split over kslot_split waves: the slot's own and, first thing after the tables, the waves of
+    // the lightest other slots (no tables: k = 1 / W = M; else the smallest tables) -- an extra wave
+    // only when there is no other slot
     SA.helper = -1;
-    SA.helper_wave = -1;
-    if (c->kslot_split) {
+    SA.n_parts = 0;
+    if (c->kslot_split >= 2) {
         int r1 = 0;
         for (int q = 0; q < SA.n_slot; ++q)
             if (SA.tab[q] > 0 && SA.r1[q] > r1) {
                 r1 = SA.r1[q];
                 SA.helper = q;
             }
-        int light = 1 << 30;
-        for (int q = 0; q < SA.n_slot && SA.helper >= 0; ++q) {
-            const int work = SA.tab[q] > 0 ? SA.r1[q] : 0;
-            if (q != SA.helper && work <= light) {  // ties: the later slot (larger k, less work)
-                light = work;
-                SA.helper_wave = q;
+    }
+    if (SA.helper >= 0) {
+        // helpers: the lightest other slots (no tables, then the smallest; ties: the later slot)
+        int used = 0;
+        for (int h = 0; h < c->kslot_split - 1; ++h) {
+            int pick = -1, light = 1 << 30;
+            for (int q = 0; q < SA.n_slot; ++q) {
+                const int work = SA.tab[q] > 0 ? SA.r1[q] : 0;
+                bool taken = q == SA.helper;
+                for (int u = 0; u < used; ++u) taken = taken || SA.part_wave[u] == q;
+                if (!taken && work <= light) {
+                    light = work;
+                    pick = q;
+                }
             }
+            if (pick < 0) break;
+            SA.part_wave[used++] = pick;
         }
-        if (SA.helper >= 0 && SA.helper_wave < 0) {
-            if (SA.n_slot < kMaxSlots) SA.helper_wave = SA.n_slot;
+        if (used == 0) {  // no other slot: one extra wave takes part 2
+            if (SA.n_slot < kMaxSlots) SA.part_wave[used++] = SA.n_slot;
             else SA.helper = -1;
         }
+        SA.n_parts = used + 1;
     }
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
@@ -652,8 +662,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->sweep_waves = sw ? std::atoi(sw) : 0;
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
-    const char *ks = std::getenv("HALDA_KSLOT_SPLIT");
-    c->kslot_split = !(ks && ks[0] == '0');
+    const char *ks = std::getenv("HALDA_KSLOT_SPLIT");  // parts of the k-slot scan split: 0 / 1 off, 2, 3
+    c->kslot_split = ks ? std::max(0, std::min(std::atoi(ks), kMaxSplitParts)) : 2;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||

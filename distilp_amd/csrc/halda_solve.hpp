@@ -956,20 +956,33 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 // false (caller runs the general scan) when a leaf is not convex / monotone.
 // On success st0 holds the allocation (table indices e_i).
 //
-// Split over two waves of a k-slot workgroup (16-lane segments only, sp != nullptr): the scan's
-// length is the workgroup's critical path, and each event is a dependent chain of reductions, so the
-// candidate range is cut at T_mid and both halves run at once. Part 1 (the slot's own wave) takes the
-// openings T <= T_mid; part 2 (the helper wave) starts from the optimal capped allocation at T_mid --
-// the state part 1 would reach there (the capped optimum is unique when no two devices tie on an
-// increment) -- and takes the rest, pruning with its own bound (never fewer events than the one scan
-// makes above T_mid). Part 1 then takes part 2's allocation when it is strictly better, so the
-// earliest T wins ties as in the one scan. T_mid = the lower median over the devices of H at
-// cap(T0) + 2 (tools/scan_model.py on dumped C2 tables: the longest scan 47 -> 28 events per wave).
+// Split over two or three waves of a k-slot workgroup (16-lane segments only, sp.part != 0): the
+// scan's length is the workgroup's critical path, and each event is a dependent chain of reductions,
+// so the candidate range is cut at T_a (and T_b) and the parts run at once. Part 1 (the slot's own
+// wave) takes the openings T <= T_a; part p > 1 (a helper wave) starts from the optimal capped
+// allocation at its lower cut -- the state the one scan reaches there (the capped optimum is unique
+// when no two devices tie on an increment) -- and takes the openings up to its upper cut, pruning with
+// its own bound (never fewer events than the one scan makes in its range). Part 1 then takes the
+// helpers' allocations in ascending T, each only when strictly better, so the earliest T wins ties as
+// in the one scan. Cuts (tools/scan_model.py on dumped C2 tables, the longest scan per wave): two
+// parts, the lower median over the devices of H at cap(T0) + 2 (47 -> 28 events); three parts, the
+// lower quartile of H at cap(T0) + 2 and the lower median of H at cap(T0) + 3 (-> 21 events).
+constexpr int kMaxSplitParts = 3;
+struct SplitArea {  // per segment, in LDS
+    // part 1 -> the helpers, after its leaf scan and phase-0 greedy (the helpers repeat neither)
+    double s_inf, best0;
+    int lo_sum, capsum;
+    int pub;             // 0: not yet, 1: published, 2: part 1 does not scan (the helpers skip)
+    int lo[16], hi[16];  // each device's finite leaf range
+    // the helpers -> part 1
+    double alt_best[kMaxSplitParts - 1];  // part p's best objective (+inf: nothing beat its start)
+    int flag[kMaxSplitParts - 1];         // set once part p's alt_e / alt_best are final
+    int alt_e[kMaxSplitParts - 1][16];    // part p's allocation (one int per segment lane)
+};
 struct ScanSplit {
-    int part = 0;                // 0: no split, 1: openings T <= T_mid, 2: T > T_mid (the helper)
-    int *alt_e = nullptr;        // part 2's allocation (one int per segment lane), LDS
-    double *alt_best = nullptr;  // part 2's best objective, +inf when nothing beat its start, LDS
-    int *flag = nullptr;         // set by the helper once alt_e / alt_best are final, LDS
+    int part = 0;     // 0: no split, 1: the slot's own wave, 2 / 3: a helper
+    int n_parts = 0;  // 2 or 3
+    SplitArea *ar = nullptr;
 };
 
 // Rank of v among the 16 lanes of its DPP row (ties: the lower lane first).
@@ -1002,24 +1015,34 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     int cap = lo;
     if (act)
         while (cap < hi && H[cap + 1] <= T) ++cap;
-    double t_mid = kInf;  // part 1 stops past it, part 2 starts there
     const int part = sp.part;
-    double t_stop = kInf;
+    double t_stop = kInf;  // the part's upper cut (inclusive)
     if constexpr (SG::S == 16) {
         if (part) {
-            const double v = act && cap < hi ? H[min(cap + 2, hi)] : kInf;
-            const int rank = rank16(v, lane, std::make_integer_sequence<int, 15>{});
-            const int n = sg.sum_i(v < kInf ? 1 : 0);
-            t_mid = sg.min_f64(v < kInf && rank == (n - 1) / 2 ? v : kInf);  // > T0; +inf: no opening at all
-            if (part == 1) t_stop = t_mid;
-            if (part == 2) {
-                T = t_mid;
+            const bool has = act && cap < hi;  // a device with an opening past T0
+            const double v2 = has ? H[min(cap + 2, hi)] : kInf;
+            const int n = sg.sum_i(has ? 1 : 0);
+            const int r2 = rank16(v2, lane, std::make_integer_sequence<int, 15>{});
+            double ta, tb = kInf;  // cuts > T0; +inf: no opening at all
+            if (sp.n_parts == 2) {
+                ta = sg.min_f64(has && r2 == (n - 1) / 2 ? v2 : kInf);
+            } else {
+                const double v3 = has ? H[min(cap + 3, hi)] : kInf;
+                const int r3 = rank16(v3, lane, std::make_integer_sequence<int, 15>{});
+                const double a = sg.min_f64(has && r2 == (n - 1) / 4 ? v2 : kInf);
+                const double b = sg.min_f64(has && r3 == (n - 1) / 2 ? v3 : kInf);
+                ta = fmin(a, b);
+                tb = fmax(a, b);
+            }
+            t_stop = part == 1 ? ta : part == 2 ? tb : kInf;
+            if (part > 1) {
+                T = part == 2 ? ta : tb;
                 if (act)
                     while (cap < hi && H[cap + 1] <= T) ++cap;
             }
         }
     }
-    // optimal capped allocation at T0 (part 2: at T_mid) (greedy: every cap filled from lo, then the smallest increments)
+    // optimal capped allocation at T0 (a helper: at its lower cut) (greedy: every cap filled from lo, then the smallest increments)
     int e = lo;
     int need = need_total;
     {
@@ -1062,9 +1085,9 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
         lam = sg.max_f64(lt);
         lj = sg.highest(lt == lam);
         if (kc * T + S < best) {
-            // part 2's start only bounds its pruning: part 1 already priced this allocation at a lower T
+            // a helper's start only bounds its pruning: a lower part already priced this allocation
             best = kc * T + S;
-            bestE = part == 2 ? -1 : e;
+            bestE = part > 1 ? -1 : e;
         }
     }
     while (true) {
@@ -1108,20 +1131,23 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     nodes += events;
     HALDA_KSTAMP(5);
     if constexpr (SG::S == 16) {
-        if (part == 2) {  // the helper: its result for part 1 (it posts the flag itself)
-            if (act && bestE >= 0) sp.alt_e[lane] = bestE;
-            if (lane == 0) *sp.alt_best = bestE >= 0 ? best : kInf;
+        if (part > 1) {  // a helper: its result for part 1 (it posts the flag itself)
+            const int h = part - 2;
+            if (act && bestE >= 0) sp.ar->alt_e[h][lane] = bestE;
+            if (lane == 0) sp.ar->alt_best[h] = bestE >= 0 ? best : kInf;
             wave_sync();
             return true;
         }
-        if (part == 1) {  // wait for the helper's half, keep the strictly better one
-            while (__hip_atomic_load(sp.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-                __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const double ab = *sp.alt_best;
-            if (ab < best) {
-                best = ab;
-                bestE = act ? sp.alt_e[lane] : 0;
+        if (part == 1) {  // the helpers' parts in ascending T, each kept only when strictly better
+            for (int h = 0; h < sp.n_parts - 1; ++h) {
+                while (__hip_atomic_load(&sp.ar->flag[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const double ab = sp.ar->alt_best[h];
+                if (ab < best) {
+                    best = ab;
+                    bestE = act ? sp.ar->alt_e[h][lane] : 0;
+                }
             }
         }
     }
@@ -1216,6 +1242,20 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
 #ifdef HALDA_STAMPS
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();  // phase-0 greedy done
 #endif
+    if (sp.part == 1) {  // the helpers start from here (kslot_helper)
+        if (act) {
+            sp.ar->lo[lane] = lo;
+            sp.ar->hi[lane] = hi;
+        }
+        if (lane == 0) {
+            sp.ar->s_inf = s_inf;
+            sp.ar->best0 = I.kc * hmax + s_inf;
+            sp.ar->lo_sum = li.lo_sum;
+            sp.ar->capsum = li.cap;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&sp.ar->pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li, sp);
     wave_sync();
     return 1;

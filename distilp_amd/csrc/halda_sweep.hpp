@@ -1355,22 +1355,24 @@ struct SlotArgs {
     int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * (R + 1) + max_devices, 0: no tables
     int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
     int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
-    int helper;                // slot whose threshold scan is split over two waves (-1: none)
-    int helper_wave;           // the wave that takes its upper half first: a light slot's, or n_slot (extra)
+    int helper;                // slot whose threshold scan is split over n_parts waves (-1: none)
+    int n_parts;               // 2 or 3
+    int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 / 3 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
 };
+static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
 
-// What the helper wave hands to the split slot's wave, per segment (kc_scan_incremental, ScanSplit).
-struct SplitArea {
-    double alt_best;
-    int flag;
-    int pad;
-    int alt_e[kSegLanes];
-};
-
-// Waves of a k-slot workgroup: one per slot, plus the helper.
+// Waves of a k-slot workgroup: one per slot, plus an extra helper wave when no other slot can host one.
 __host__ __device__ inline int kslot_waves(const SlotArgs &SA) {
-    return SA.n_slot + (SA.helper >= 0 && SA.helper_wave == SA.n_slot ? 1 : 0);
+    return SA.n_slot + (SA.helper >= 0 && SA.part_wave[0] == SA.n_slot ? 1 : 0);
+}
+
+// Part (2 or 3) of the split scan this wave takes first, 0: none.
+__device__ inline int kslot_part_of(const SlotArgs &SA, int q) {
+    if (SA.helper < 0) return 0;
+    for (int h = 0; h < SA.n_parts - 1; ++h)
+        if (SA.part_wave[h] == q) return h + 2;
+    return 0;
 }
 
 // One (fleet, k_j) on a 16-lane segment; the result goes to *pk (segment lane 0 writes obj / st, lane i
@@ -1649,31 +1651,59 @@ __device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const 
     }
 }
 
-// The helper wave of a k-slot workgroup: the upper half (T > T_mid) of the split slot's threshold scan
-// for its segment's fleet -- the same leaf scan and phase-0 greedy as the slot's own wave, then
-// kc_scan_incremental part 2 into the split area -- and the flag, on every path (the slot's wave
-// waits for it only when its own scan ran to the end).
-__device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const KslotFleet &fd, SplitArea *ar,
-                             const Seg<kSegLanes> &sg, unsigned char *smem, int seg) {
-    const int p = SA.helper;
+// A helper wave of a k-slot workgroup, after its own slot: its part (T range) of the split slot's
+// threshold scan for its segment's fleet, from what part 1 published after its leaf scan and phase-0
+// greedy (part 1 publishes on every path: "skip" when it does not scan), into the split area; then
+// the flag, on every path (part 1 waits for it only when it scanned). The wait is a wave-uniform
+// polling loop in which every segment whose publication is in runs its part at once: a segment must
+// never wait behind another one of the same wave (part 1 may publish that one only after its own
+// scan, which waits for this segment's flag).
+__device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const KslotFleet &fd, SplitArea *ar, int part,
+                             const Seg<kSegLanes> &sg, unsigned char *smem, int seg, bool live) {
+    const int p = SA.helper, h = part - 2, lane = sg.sl;
     const int j = SA.j[p], k = A.ks[j], W = A.Ws[j];
-    if (sg.sl == 0) ar->alt_best = kInf;
-    if (kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) {
-        Inst I = {};
-        I.M = fd.M;
-        I.W = W;
-        I.Wd = double(W);
-        I.kc = double(k - 1);
-        I.iC = 7 * fd.M;
-        I.R1 = W - fd.M + 1;
-        I.RS = odd_stride(I.R1);
-        WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
-        w.st0 = ar->alt_e;  // the phase-0 allocation and part 2's result, not the slot's st0
-        int64_t nodes = 0;
-        (void)dp_pass_lanes(w, I, sg, nodes, nullptr, ScanSplit{2, ar->alt_e, &ar->alt_best, &ar->flag});
+    // part 1 reaches its leaf scan (else it publishes nothing this wave needs: post at once)
+    bool pending = live && kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax);
+    if (live && lane == 0) ar->alt_best[h] = kInf;
+    while (__ballot(pending)) {
+        const int pb = pending ? __hip_atomic_load(&ar->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+        if (pending && pb != 0) {  // segment-uniform
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (pb == 1) {
+                Inst I = {};
+                I.M = fd.M;
+                I.W = W;
+                I.Wd = double(W);
+                I.kc = double(k - 1);
+                I.iC = 7 * fd.M;
+                I.R1 = W - fd.M + 1;
+                I.RS = odd_stride(I.R1);
+                const bool act = lane < fd.M;
+                LeafInfo li = {};
+                li.convex = true;  // part 1 checked every leaf before it published
+                li.mono = true;
+                li.empty = false;
+                li.lo_sum = ar->lo_sum;
+                li.cap = ar->capsum;
+                li.my_lo = act ? ar->lo[lane] : 0;
+                li.my_hi = act ? ar->hi[lane] : -1;
+                WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
+                w.st0 = ar->alt_e[h];  // this part's result, not the slot's st0
+                int64_t nodes = 0;
+                (void)kc_scan_incremental(w, I, sg, ar->s_inf, ar->best0, nodes, li,
+                                          ScanSplit{part, SA.n_parts, ar});
+            }
+            pending = false;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&ar->flag[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (pending) {
+            __builtin_amdgcn_s_sleep(2);
+        }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (sg.sl == 0) __hip_atomic_store(&ar->flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (live && !kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&ar->flag[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 }
 
 __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
@@ -1686,18 +1716,19 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     const int nf = A.F.n_fleets;
     const int64_t f = int64_t(blockIdx.x) * kPer + seg;
     SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
+    // the slot with the largest k > 1 tables (C2: k = 2) is the workgroup's critical path: its
+    // threshold scan is the last thing running. It gets the SIMD's issue priority over the other
+    // slots' waves (of other workgroups) it shares the SIMD with.
+    int crit = -1;
     {
-        // the slot with the largest k > 1 tables (C2: k = 2) is the workgroup's critical path: its
-        // threshold scan is the last thing running. It gets the SIMD's issue priority over the other
-        // slots' waves (of other workgroups) it shares the SIMD with.
-        int crit = -1, r1 = 0;
+        int r1 = 0;
         for (int p = 0; p < SA.n_slot; ++p)
             if (SA.tab[p] > 0 && SA.r1[p] > r1) {
                 r1 = SA.r1[p];
                 crit = p;
             }
-        if (q == crit || (SA.helper >= 0 && q == SA.helper_wave)) __builtin_amdgcn_s_setprio(3);  // and its helper
     }
+    if (q == crit) __builtin_amdgcn_s_setprio(3);  // (its helpers once their own slot is done)
     SplitArea *split = reinterpret_cast<SplitArea *>(smem + SA.split_off) + seg;
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
@@ -1710,16 +1741,17 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         if (f < nf) fd = kslot_records(A, int(f), sg);
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
         if (f < nf) kslot_tables(A, SA, q, fd, sg, smem, seg);
-        if (SA.helper >= 0 && q == SA.helper_wave && sg.sl == 0) split->flag = 0;  // posted after the barrier
+        const int my_part = kslot_part_of(SA, q);
+        if (my_part && sg.sl == 0) split->flag[my_part - 2] = 0;  // posted after the barrier
+        if (q == SA.helper && sg.sl == 0) split->pub = 0;
         HALDA_KSTAMPW(6, __builtin_amdgcn_s_memtime());
         __syncthreads();  // every slot's tables are complete
         HALDA_KSTAMPW(11, __builtin_amdgcn_s_memtime());
-        if (SA.helper >= 0 && q == SA.helper_wave) {  // the helper's half first: the split slot waits for it
-            if (f < nf) kslot_helper(A, SA, fd, split, sg, smem, seg);
-            if (q == SA.n_slot) {  // an extra wave: no slot of its own
-                __syncthreads();   // the pick barrier below
-                return;
-            }
+        if (q == SA.n_slot) {  // an extra helper wave: no slot of its own
+            __builtin_amdgcn_s_setprio(3);
+            kslot_helper(A, SA, fd, split, my_part, sg, smem, seg, f < nf);
+            __syncthreads();  // the pick barrier below
+            return;
         }
         const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
 #ifdef HALDA_STAMPS
@@ -1733,9 +1765,14 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         }
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
-        const ScanSplit sp{q == SA.helper ? 1 : 0, split->alt_e, &split->alt_best, &split->flag};
+        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split};
         if (f < nf)
             sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
+        if (q == SA.helper && f < nf && sg.sl == 0 && split->pub == 0) split->pub = 2;  // did not scan: helpers skip
+        if (my_part) {  // after its own slot, at the split slot's priority
+            __builtin_amdgcn_s_setprio(3);
+            kslot_helper(A, SA, fd, split, my_part, sg, smem, seg, f < nf);
+        }
         HALDA_KSTAMPW(7, t_rec[2]);
         HALDA_KSTAMPW(8, t_rec[3]);
         HALDA_KSTAMPW(9, t_rec[4]);
