@@ -78,6 +78,8 @@ struct Ctx {
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     int kslot_split = 2;                         // k-slot launch: the longest scan split over this many waves
+    int kslot_split_env = 2;                     // its value from HALDA_KSLOT_SPLIT (fleets path 1 restores it)
+    int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters)
     int sweep_waves = 0;                         // > 0: the register launch as the pipelined kernel, this many waves
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
@@ -430,6 +432,7 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         }
         SA.n_parts = used + 1;
     }
+    SA.crit_w4 = c->kslot_crit_w4;
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
     if (SA.helper >= 0) kslot_lds += int64_t(64 / kSegLanes) * int64_t(sizeof(SplitArea));
@@ -664,6 +667,9 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->xcd_swizzle = !(xs && xs[0] == '0');
     const char *ks = std::getenv("HALDA_KSLOT_SPLIT");  // parts of the k-slot scan split: 0 / 1 off, 2, 3
     c->kslot_split = ks ? std::max(0, std::min(std::atoi(ks), kMaxSplitParts)) : 2;
+    c->kslot_split_env = c->kslot_split;
+    const char *cw = std::getenv("HALDA_KSLOT_CRIT_W");
+    c->kslot_crit_w4 = cw ? std::max(1, std::min(std::atoi(cw), 16)) : 10;  // 2.5x (measured best of 4..12)
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
@@ -764,13 +770,15 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
 int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    if (path < 0 || path > 4)
+    if (path < 0 || path > 6)
         return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave), 3 (fused, k = 1 "
-                                 "by DP) or 4 (fused, segment kernel instead of the k-slot kernel)");
+                                 "by DP), 4 (fused, segment kernel instead of the k-slot kernel), 5 / 6 (fused, "
+                                 "the k-slot scan unsplit / in three parts)");
     c->fleets_fused = path != 0;
-    c->seg_sweep = path == 1 || path == 4;
-    c->kslot_sweep = path == 1;
+    c->seg_sweep = path == 1 || path == 4 || path == 5 || path == 6;
+    c->kslot_sweep = path == 1 || path == 5 || path == 6;
     c->k1_force_dp = path == 3;
+    c->kslot_split = path == 5 ? 0 : path == 6 ? 3 : c->kslot_split_env;
     return HALDA_OK;
 }
 

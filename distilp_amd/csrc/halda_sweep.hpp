@@ -1359,6 +1359,7 @@ struct SlotArgs {
     int n_parts;               // 2 or 3
     int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 / 3 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
+    int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
 };
 static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
 
@@ -1427,13 +1428,18 @@ __device__ inline WaveCtx kslot_ctx(const SweepArgs &A, const SlotArgs &SA, int 
 // stretch starts with a full split search, the same least minimisers as one chain, so the same
 // tables), instead of each k > 1 wave building its own while the W = M / k = 1 waves idle at the
 // barrier: the longest wave's dependent chain loses its table pass.
-__device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, const KslotFleet &fd,
+__device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, int crit, const KslotFleet &fd,
                              const Seg<kSegLanes> &sg, unsigned char *smem, int seg) {
     const int lane = sg.sl;
     int total = 0;
     for (int p = 0; p < SA.n_slot; ++p) total += SA.tab[p] > 0 ? SA.r1[p] : 0;
     const int nw = kslot_waves(SA);
-    const int lo = q * total / nw, hi = (q + 1) * total / nw;
+    // wave weights in quarters: 4 each, crit_w4 for the critical slot's wave (issue priority: it
+    // builds faster and would otherwise wait at the barrier)
+    const int cw = crit >= 0 ? SA.crit_w4 : 4;
+    const int64_t wt = 4 * int64_t(nw) + cw - 4;
+    auto before = [&](int r) { return 4 * int64_t(r) + (crit >= 0 && crit < r ? cw - 4 : 0); };
+    const int lo = int(total * before(q) / wt), hi = int(total * before(q + 1) / wt);
     int base = 0;
     for (int p = 0; p < SA.n_slot; ++p) {
         if (SA.tab[p] <= 0) continue;
@@ -1740,7 +1746,7 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         KslotFleet fd = {};
         if (f < nf) fd = kslot_records(A, int(f), sg);
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
-        if (f < nf) kslot_tables(A, SA, q, fd, sg, smem, seg);
+        if (f < nf) kslot_tables(A, SA, q, crit, fd, sg, smem, seg);
         const int my_part = kslot_part_of(SA, q);
         if (my_part && sg.sl == 0) split->flag[my_part - 2] = 0;  // posted after the barrier
         if (q == SA.helper && sg.sl == 0) split->pub = 0;
