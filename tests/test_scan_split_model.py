@@ -1,0 +1,44 @@
+"""The k-slot kernel's split threshold scan (ScanSplit, distilp_amd/csrc/halda_solve.hpp), as an
+algorithm: on random tables of the shape the scan accepts (convex G rows, nondecreasing H rows), the
+parts cut at the kernel's T_a (T_b) and merged the kernel's way (a later part only when strictly
+better) find the one scan's optimum, which is the brute-force min over T of kc T + S(T)
+(tools/scan_model.py restates the kernel's scan; the GPU kernel itself is checked bit for bit against
+the unsplit sweep in test_gpu_sweep.py)."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+import scan_model as sm  # noqa: E402
+
+
+def _tables(rng, M, R1):
+    """Convex G rows (increasing increments) and nondecreasing H rows, some rows with a finite prefix."""
+    G = np.full((M, R1), np.inf)
+    H = np.full((M, R1), np.inf)
+    for i in range(M):
+        n = R1 if rng.random() < 0.8 else int(rng.integers(R1 // 2, R1))
+        inc = np.sort(rng.uniform(0.01, 1.0, n - 1))
+        G[i, :n] = rng.uniform(0.0, 1.0) + np.concatenate([[0.0], np.cumsum(inc)])
+        H[i, :n] = rng.uniform(0.05, 0.3) + np.cumsum(rng.uniform(0.0, 0.1, n))
+    return G, H
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_split_parts_merge_to_the_one_scan(seed):
+    rng = np.random.default_rng(seed)
+    Gs, Hs = [], []
+    for _ in range(24):
+        g, h = _tables(rng, 12, 20)
+        Gs.append(g)
+        Hs.append(h)
+    G, H = np.array(Gs), np.array(Hs)
+    rep = sm.split_report(G, H, len(Gs), kc=1.0)
+    for parts, (longest, _, agree) in rep.items():
+        assert agree, parts
+    assert rep[1][0] > 0 and rep[2][0] <= rep[1][0] and rep[3][0] <= rep[1][0]  # the scans do run
+    for f in range(len(Gs)):  # the one scan is the brute-force optimum
+        r = sm.model(G[f], H[f], 1.0, 0)
+        assert abs(r["best"] - r["brute"]) <= 1e-9 * max(1.0, abs(r["brute"]))
