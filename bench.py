@@ -483,7 +483,7 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
         "ms_per_step_one_stream": ev1, "instances_per_s_one_stream": inst / (ev1 * 1e-3),
         "ms_per_step_two_streams": el2 / steps * 1e3, "instances_per_s_two_streams": inst * steps / el2,
         "steps": steps, "resident_copies": n,
-        "roofline": roofline(ph, {k: alg for k in ph}, lambda k: None, ev1 if single_launch_steps(ph) else None,
+        "roofline": roofline(ph, {k: alg for k in ph}, pmc_traffic, ev1 if single_launch_steps(ph) else None,
                              workload="c2"),
     }
 
