@@ -444,6 +444,8 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     table = fleet_table(build_fleets(range(C3_FLEETS), M2), model)
     n = max(2, min(32, math.ceil(2 * MALL_BYTES / max(DeviceFleetTable(table, model, KS_L80, 0.5, dev).nbytes(), 1))))
     tabs = [DeviceFleetTable(table, model, KS_L80, 0.5, dev, want_per_k=True) for _ in range(n)]
+    for t in tabs:
+        t.plan(ctx)
     turn = [0]
 
     def step2():
@@ -455,8 +457,12 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
         turn[0] += 1
 
     ctx.set_timing(False)
+    # warm every stream the leg uses with the leg's own launch (each stream's scratch slot is grown to
+    # this batch here, not inside a timed region)
     for _ in range(max(2, args.warmup)):
         step1()
+    for _ in range(2 * len(srefs)):
+        step2()
     torch.cuda.synchronize(dev)
     st = tabs[(turn[0] - 1) % n].out["status"].cpu().numpy()
     n_opt = int((st == 0).sum())
@@ -621,8 +627,12 @@ def main():
 
     setup_s = time.perf_counter() - t_setup
 
-    # warm-up and sanity: the sweep's per-fleet answers equal the solve-only leg's k = 1 solves
-    for _ in range(args.warmup):
+    # prepared launches (halda_fleets_plan_create) are set-up, not steps
+    for t in sweeps:
+        t.plan(ctx)
+    # warm-up and sanity: the sweep's per-fleet answers equal the solve-only leg's k = 1 solves (at least
+    # one warm-up step per stream, so that no stream meets its first launch inside a timed region)
+    for _ in range(max(args.warmup, len(srefs))):
         sweep_step()
         solve_step()
     torch.cuda.synchronize(dev)
@@ -646,13 +656,15 @@ def main():
         s_table = fleet_table(build_fleets(s_seeds, args.M), model)
         n_st = max(2, min(32, math.ceil(2 * MALL_BYTES / max(DeviceFleetTable(s_table, model, ks, 0.5, dev).nbytes(), 1))))
         s_sweeps = [DeviceFleetTable(s_table, model, ks, 0.5, dev) for _ in range(n_st)]
+        for t in s_sweeps:
+            t.plan(ctx)
         sturn = [0]
 
         def strong_step():
             s_sweeps[sturn[0] % n_st].launch(ctx, srefs[sturn[0] % len(srefs)])
             sturn[0] += 1
 
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, len(srefs))):
             strong_step()
         el_strong = timed(strong_step, args.steps, torch, dev, dist, world)
 

@@ -80,7 +80,6 @@ struct Ctx {
     int kslot_split = 2;                         // k-slot launch: the longest scan split over this many waves
     int kslot_split_env = 2;                     // its value from HALDA_KSLOT_SPLIT (fleets path 1 restores it)
     int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters)
-    int sweep_waves = 0;                         // > 0: the register launch as the pipelined kernel, this many waves
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
@@ -89,6 +88,8 @@ struct Ctx {
     bool last_fleet_fused = false;
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
     size_t shard_bytes = 0;
+    void *emu = nullptr;           // the other virtual ranks' results of halda_solve_fleets_sharded_emulated
+    size_t emu_bytes = 0;
     // The fused sweep's scratch (per-fleet "needs the table launch" bytes, the hand-back flag) per
     // stream: launches on one stream are ordered by it, so batches enqueued on different streams use
     // different slots and need no cross-stream ordering (they overlap on the device). A slot moving to
@@ -351,8 +352,28 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
 // budget, the register launch plus the global-table launch.
 constexpr int kSweepSmallBatch = 64;
 
-int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
-                 const halda_fleet_result &out, hipStream_t s) {
+// The fused sweep's launch sequence for one batch shape, derived from the shapes alone (no HIP call):
+// which kernels, their grids and LDS slices, and the kernel arguments but for the per-launch scratch
+// fields (fflag, hb_flag, launch_id, want), which run_sweep fills. sweep_fleets plans and runs in one
+// go; a prepared plan (halda_fleets_plan_create) is planned once and run per launch.
+enum SweepKind { kRegAlone, kRegGated, kRegBig, kTablesAlone, kSegGated, kKslotGated };
+
+struct SweepPlan {
+    SweepArgs A;
+    SlotArgs SA;
+    SweepKind kind;
+    bool scratch;      // per-fleet flags / hand-back flag of the stream's slot in use
+    int nf;
+    int64_t lds;       // the first launch's dynamic LDS (k-slot / segment / table kernel)
+    int64_t slice;     // the table kernel's LDS slice
+    unsigned grid1;    // the first launch's grid
+    unsigned block1;   // its workgroup size
+    unsigned grid2;    // the gated second launch's grid (0: none)
+    const void *fn1;   // first kernel (for the occupancy / LDS attribute)
+};
+
+int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
+               const halda_fleet_result &out, SweepPlan *P) {
     const int nf = F.n_fleets;
     int64_t r1_k1 = 0, r1_kc = 0;
     for (int j = 0; j < n_k; ++j) {
@@ -447,13 +468,12 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
     // the register launch flags k > 1 / wide fleets (tables_first) and k = 1 greedy fallbacks with
     // R + 1 > kDpLanes; the others it solves itself (k1_dp), so no table launch is needed without them
     const bool gate = tables_first || r1_k1 > kDpLanes;
-    const bool scratch = !(reg_mode && !gate);  // flags / hand-back flag of this stream's slot in use
-    Ctx::SweepSlot *slot = nullptr;
-    if (scratch) {
-        const int rc = sweep_slot(c, s, nf, &slot);
-        if (rc != HALDA_OK) return rc;
-    }
-    SweepArgs A = {};
+    SweepPlan &p = *P;
+    p = SweepPlan{};
+    p.nf = nf;
+    p.slice = slice;
+    p.scratch = !(reg_mode && !gate);
+    SweepArgs &A = p.A;
     A.Mo = model;
     A.F = F;
     for (int j = 0; j < n_k; ++j) {
@@ -466,82 +486,104 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
              (c->x_zero ? kOutXZ : 0);
     A.x_off = out.x_off;
     A.xstride = 7 * int64_t(std::max(mmax, 1)) + 1;
-    A.fflag = scratch ? slot->fflag : nullptr;
-    A.hb_flag = scratch ? slot->hb : c->hb_flag;
-    A.launch_id = ++c->launch_id;
     A.mmax = mmax;
     A.uM = F.min_devices == F.max_devices ? F.max_devices : 0;
     A.k1dp = c->k1_force_dp ? 1 : 0;
     A.r1max = int(r1max);
     A.tab = int(tab);
     A.tab_kc = int(tab_kc);
-    c->fleet_timed = false;
-    c->have_lowered = false;
-    if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
+    p.SA = SA;
+    const unsigned cap_cus = unsigned(std::min<int64_t>(c->cus, nf));
     if (kslot) {
-        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_kslot_kernel), kslot_lds, nullptr));
-        const int64_t groups = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
-        A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_kslot_kernel, dim3(unsigned(groups)), dim3(64 * kslot_waves(SA)),
-                           size_t(kslot_lds), s, A, SA);
-        HIP_TRY(hipGetLastError());
-        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
-        A.want = 1;
-        int per_cu = 0;
-        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(unsigned(std::min<int64_t>(c->cus, nf))), dim3(64),
-                           size_t(slice), s, A);
-        HIP_TRY(hipGetLastError());
+        p.kind = kKslotGated;
+        p.fn1 = reinterpret_cast<const void *>(halda_sweep_kslot_kernel);
+        p.lds = kslot_lds;
+        p.grid1 = unsigned((int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes));
+        p.block1 = unsigned(64 * kslot_waves(SA));
+        p.grid2 = cap_cus;
     } else if (seg) {
+        p.kind = kSegGated;
+        p.fn1 = reinterpret_cast<const void *>(halda_sweep_seg_kernel);
+        p.lds = seg_lds;
         int per_cu = 0;
-        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_seg_kernel), seg_lds, &per_cu));
+        HIP_TRY(c->occupancy(p.fn1, seg_lds, &per_cu));
         const int64_t nw = (int64_t(nf) + 64 / kSegLanes - 1) / (64 / kSegLanes);
-        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nw)));
-        A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_seg_kernel, dim3(grid), dim3(64), size_t(seg_lds), s, A);
-        HIP_TRY(hipGetLastError());
-        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
-        A.want = 1;
-        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(unsigned(std::min<int64_t>(c->cus, nf))), dim3(64),
-                           size_t(slice), s, A);
-        HIP_TRY(hipGetLastError());
+        p.grid1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nw)));
+        p.block1 = 64;
+        p.grid2 = cap_cus;
     } else if (fits && (tables_first || small_tables)) {
         // small batches (a single halda_solve): one launch with the table slice instead of two
+        p.kind = kTablesAlone;
+        p.fn1 = reinterpret_cast<const void *>(halda_sweep_tables_kernel);
+        p.lds = slice;
         int per_cu = 0;
-        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
-        A.want = 0;
-        hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(c->occupancy(p.fn1, slice, &per_cu));
+        p.grid1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(int64_t(c->cus) * per_cu, nf)));
+        p.block1 = 64;
     } else {
-        A.want = 0;
-        const int pipe_waves = c->sweep_waves > 0 && A.uM > 0 && A.uM <= kK1MaxM && nf > c->sweep_waves ? c->sweep_waves : 0;
-        if (pipe_waves > 0) {
-            hipLaunchKernelGGL(halda_sweep_pipe_kernel,
-                               dim3(unsigned((pipe_waves + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
-                               dim3(64 * kSweepWavesPerBlock), 0, s, A, pipe_waves);
-        } else {
-            hipLaunchKernelGGL(halda_sweep_kernel, dim3(unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock)),
-                               dim3(64 * kSweepWavesPerBlock), 0, s, A);
-        }
-        HIP_TRY(hipGetLastError());
-        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
-        A.want = 1;  // the fleets flagged above, gated on the hand-back flag
+        p.fn1 = reinterpret_cast<const void *>(halda_sweep_kernel);
+        p.grid1 = unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock);
+        p.block1 = 64 * kSweepWavesPerBlock;
         if (!gate) {
+            p.kind = kRegAlone;
         } else if (fits) {  // flagged fleets are rare (fast-path fallbacks): one wave per CU is plenty
+            p.kind = kRegGated;
             int per_cu = 0;
             HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, &per_cu));
-            int grid = int(std::max<int64_t>(1, std::min<int64_t>(tables_first ? int64_t(c->cus) * per_cu
-                                                                             : int64_t(c->cus), nf)));
-            hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(grid), dim3(64), size_t(slice), s, A);
+            p.grid2 = unsigned(std::max<int64_t>(1, std::min<int64_t>(tables_first ? int64_t(c->cus) * per_cu
+                                                                                   : int64_t(c->cus), nf)));
         } else {
+            p.kind = kRegBig;
             A.gstride = (slice + 255) & ~int64_t(255);
             int per_cu = 0;
             HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_big_kernel), 0, &per_cu));
-            const int grid = int(std::max<int64_t>(
+            p.grid2 = unsigned(std::max<int64_t>(
                 1, std::min<int64_t>({int64_t(c->cus) * per_cu, int64_t(nf), kGlobalTableBudget / A.gstride})));
-            const size_t gneed = size_t(A.gstride) * size_t(grid);
+        }
+    }
+    if (p.kind == kKslotGated) HIP_TRY(c->occupancy(p.fn1, p.lds, nullptr));
+    if (p.kind == kKslotGated || p.kind == kSegGated)
+        HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, nullptr));
+    return HALDA_OK;
+}
+
+// Enqueue a planned sweep on stream s: the stream's scratch slot (when the plan uses scratch), the
+// first launch and the gated table launch behind it (global tables: after the previous launch on them).
+int run_sweep(Ctx *c, SweepPlan &p, hipStream_t s) {
+    SweepArgs &A = p.A;
+    Ctx::SweepSlot *slot = nullptr;
+    if (p.scratch) {
+        const int rc = sweep_slot(c, s, p.nf, &slot);
+        if (rc != HALDA_OK) return rc;
+    }
+    A.fflag = p.scratch ? slot->fflag : nullptr;
+    A.hb_flag = p.scratch ? slot->hb : c->hb_flag;
+    A.launch_id = ++c->launch_id;
+    A.want = 0;
+    c->fleet_timed = false;
+    c->have_lowered = false;
+    if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
+    switch (p.kind) {
+        case kKslotGated:
+            hipLaunchKernelGGL(halda_sweep_kslot_kernel, dim3(p.grid1), dim3(p.block1), size_t(p.lds), s, A, p.SA);
+            break;
+        case kSegGated:
+            hipLaunchKernelGGL(halda_sweep_seg_kernel, dim3(p.grid1), dim3(p.block1), size_t(p.lds), s, A);
+            break;
+        case kTablesAlone:
+            hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(p.grid1), dim3(p.block1), size_t(p.lds), s, A);
+            break;
+        default:
+            hipLaunchKernelGGL(halda_sweep_kernel, dim3(p.grid1), dim3(p.block1), 0, s, A);
+            break;
+    }
+    HIP_TRY(hipGetLastError());
+    const bool two = p.kind == kKslotGated || p.kind == kSegGated || p.kind == kRegGated || p.kind == kRegBig;
+    if (two) {
+        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
+        A.want = 1;  // the fleets flagged above, gated on the hand-back flag
+        if (p.kind == kRegBig) {
+            const size_t gneed = size_t(A.gstride) * size_t(p.grid2);
             if (gneed > c->gtab_bytes) {
                 if (c->gtab) HIP_TRY(hipFree(c->gtab));
                 c->gtab = nullptr;
@@ -549,8 +591,14 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
                 HIP_TRY(hipMalloc(&c->gtab, gneed));
                 c->gtab_bytes = gneed;
             }
+            // the global tables are per context (not per stream slot: up to 2 GiB each), so this launch
+            // runs after the previous user of them on another stream (a sweep's or launch()'s big launch)
+            const int rc = order_after_previous(c, s);
+            if (rc != HALDA_OK) return rc;
             A.gtab = static_cast<unsigned char *>(c->gtab);
-            hipLaunchKernelGGL(halda_sweep_big_kernel, dim3(grid), dim3(64), 0, s, A);
+            hipLaunchKernelGGL(halda_sweep_big_kernel, dim3(p.grid2), dim3(64), 0, s, A);
+        } else {
+            hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(p.grid2), dim3(64), size_t(p.slice), s, A);
         }
         HIP_TRY(hipGetLastError());
     }
@@ -558,12 +606,20 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = seg || kslot || (reg_mode && gate);
-    c->fleet_reg_alone = reg_mode && !gate;
-    c->fleet_seg = seg;
-    c->fleet_kslot = kslot;
+    c->fleet_two = two;
+    c->fleet_reg_alone = p.kind == kRegAlone;
+    c->fleet_seg = p.kind == kSegGated;
+    c->fleet_kslot = p.kind == kKslotGated;
     c->last_fleet_fused = true;
     return HALDA_OK;
+}
+
+int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
+                 const halda_fleet_result &out, hipStream_t s) {
+    SweepPlan p;
+    const int rc = plan_sweep(c, model, F, kh, n_k, out, &p);
+    if (rc != HALDA_OK) return rc;
+    return run_sweep(c, p, s);
 }
 
 // ---------------------------------------------------------------- latency mode over RCCL
@@ -618,6 +674,146 @@ int nccl_fail(ncclResult_t r, const char *what) {
         if (r_ != ncclSuccess) return nccl_fail(r_, #expr); \
     } while (0)
 
+// The steps of latency mode, shared by the RCCL entry (one rank: this process's) and the one-device
+// emulation of `world` ranks (tests, bench): per rank the sub-sweep of its k's and halda_shard_kernel
+// mode 0, all-reduce MIN obj_value, mode 1, all-reduce MIN best_k, mode 2, then (one RCCL group) SUM w,
+// SUM n, MIN obj_by_k, MAX status, and the final kernel. `ar(field, count)` performs one all-reduce (or
+// opens / closes the group) over the ranks' `o` arrays.
+enum ShardField { kShObj, kShBestK, kShGroupStart, kShW, kShN, kShObk, kShSt, kShGroupEnd };
+
+struct ShardRank {
+    int rank = 0;
+    halda_fleet_result o = {};    // this rank's copy of the full result
+    halda_fleet_result sub = {};  // its sub-sweep's results (its k's only)
+    std::vector<int32_t> mine;    // ks[rank], ks[rank + world], ...
+};
+
+constexpr int kEmuMaxWorld = 16;
+struct EmuReduce {
+    int world;
+    int field;
+    int64_t count;
+    void *p[kEmuMaxWorld];
+};
+
+// One emulated all-reduce: element i of every virtual rank's buffer becomes the MIN / SUM / MAX over
+// the ranks (the RCCL operation of that field), in place.
+__global__ __launch_bounds__(256) void halda_emu_allreduce_kernel(EmuReduce E) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= E.count) return;
+    if (E.field == kShObj || E.field == kShObk) {
+        double m = static_cast<const double *>(E.p[0])[i];
+        for (int r = 1; r < E.world; ++r) {
+            const double v = static_cast<const double *>(E.p[r])[i];
+            m = v < m ? v : m;
+        }
+        for (int r = 0; r < E.world; ++r) static_cast<double *>(E.p[r])[i] = m;
+    } else {
+        int32_t m = static_cast<const int32_t *>(E.p[0])[i];
+        for (int r = 1; r < E.world; ++r) {
+            const int32_t v = static_cast<const int32_t *>(E.p[r])[i];
+            m = E.field == kShBestK ? (v < m ? v : m) : E.field == kShSt ? (v > m ? v : m) : m + v;
+        }
+        for (int r = 0; r < E.world; ++r) static_cast<int32_t *>(E.p[r])[i] = m;
+    }
+}
+
+// Devices in the batch: n_fleets * M for one fleet size, else dev_off[n_fleets] read back (synchronous).
+int shard_device_count(const halda_fleets &F, hipStream_t s, int64_t *nd) {
+    const int64_t nf = F.n_fleets;
+    *nd = nf * F.max_devices;
+    if (F.min_devices != F.max_devices) {
+        HIP_TRY(hipMemcpyAsync(nd, F.dev_off + nf, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return HALDA_OK;
+}
+
+template <class AR>
+int shard_steps(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *ks, int n_k, int world,
+                std::vector<ShardRank> &R, hipStream_t s, AR &&ar) {
+    const halda_fleet_result &out = R[0].o;
+    if (out.x || out.c) return fail(HALDA_E_ARG, "halda_solve_fleets_sharded: x / c are not gathered (pass NULL)");
+    if (!out.best_k || !out.obj_value || !out.w || !out.n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
+    const int64_t nf = F.n_fleets;
+    if (nf <= 0) return HALDA_OK;
+    if (n_k <= 0 || n_k > 1024) return fail(HALDA_E_ARG, "n_k must be in 1..1024");
+    for (int j = 0; j < n_k; ++j)
+        if (ks[j] < 1 || (j && ks[j] <= ks[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    int64_t nd = 0;
+    {
+        const int rc = shard_device_count(F, s, &nd);
+        if (rc != HALDA_OK) return rc;
+    }
+    // rank-local sub-sweep results in the context's shard scratch (one block per rank state)
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    std::vector<size_t> o_bk, o_obj, o_w, o_n, o_obk, o_st;
+    for (auto &r : R) {
+        r.mine.clear();
+        for (int j = r.rank; j < n_k; j += world) r.mine.push_back(ks[j]);  // as halda_solve_distributed deals them
+        const size_t nsub = std::max<size_t>(r.mine.size(), 1);
+        o_bk.push_back(take(4 * nf));
+        o_obj.push_back(take(8 * nf));
+        o_w.push_back(take(4 * size_t(nd)));
+        o_n.push_back(take(4 * size_t(nd)));
+        o_obk.push_back(take(8 * nf * nsub));
+        o_st.push_back(take(4 * nf * nsub));
+    }
+    if (off > c->shard_bytes) {
+        if (c->shard) HIP_TRY(hipFree(c->shard));
+        c->shard = nullptr;
+        c->shard_bytes = 0;
+        HIP_TRY(hipMalloc(&c->shard, off));
+        c->shard_bytes = off;
+    }
+    char *base = static_cast<char *>(c->shard);
+    for (size_t i = 0; i < R.size(); ++i) {
+        halda_fleet_result &sub = R[i].sub;
+        sub = {};
+        sub.best_k = reinterpret_cast<int32_t *>(base + o_bk[i]);
+        sub.obj_value = reinterpret_cast<double *>(base + o_obj[i]);
+        sub.w = reinterpret_cast<int32_t *>(base + o_w[i]);
+        sub.n = reinterpret_cast<int32_t *>(base + o_n[i]);
+        sub.obj_by_k = out.obj_by_k ? reinterpret_cast<double *>(base + o_obk[i]) : nullptr;
+        sub.status = out.status ? reinterpret_cast<int32_t *>(base + o_st[i]) : nullptr;
+    }
+    {
+        const int rc = order_after_previous(c, s);  // the shard scratch is per context
+        if (rc != HALDA_OK) return rc;
+    }
+    for (auto &r : R)
+        if (!r.mine.empty()) {
+            const int rc = halda_solve_fleets(c, &model, &F, r.mine.data(), int32_t(r.mine.size()), &r.sub, s);
+            if (rc != HALDA_OK) return rc;
+        }
+    auto modes = [&](int mode) -> int {
+        for (auto &r : R) {
+            hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, mode, int(n_k),
+                               int(r.mine.size()), r.rank, world, F.dev_off, r.sub, r.o);
+            HIP_TRY(hipGetLastError());
+        }
+        return HALDA_OK;
+    };
+    int rc = modes(0);
+    if (rc == HALDA_OK) rc = ar(kShObj, size_t(nf));
+    if (rc == HALDA_OK) rc = modes(1);
+    if (rc == HALDA_OK) rc = ar(kShBestK, size_t(nf));
+    if (rc == HALDA_OK) rc = modes(2);
+    if (rc == HALDA_OK) rc = ar(kShGroupStart, 0);
+    if (rc == HALDA_OK) rc = ar(kShW, size_t(nd));
+    if (rc == HALDA_OK) rc = ar(kShN, size_t(nd));
+    if (rc == HALDA_OK && out.obj_by_k) rc = ar(kShObk, size_t(nf) * n_k);
+    if (rc == HALDA_OK && out.status) rc = ar(kShSt, size_t(nf) * n_k);
+    if (rc == HALDA_OK) rc = ar(kShGroupEnd, 0);
+    if (rc != HALDA_OK) return rc;
+    for (auto &r : R) {
+        hipLaunchKernelGGL(halda_shard_final_kernel, dim3(unsigned((nf + 255) / 256)), dim3(256), 0, s, int(nf), r.o);
+        HIP_TRY(hipGetLastError());
+    }
+    return HALDA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -661,8 +857,6 @@ int halda_init(int device_ordinal, void **ctx_out) {
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
-    const char *sw = std::getenv("HALDA_SWEEP_WAVES");
-    c->sweep_waves = sw ? std::atoi(sw) : 0;
     const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
     c->xcd_swizzle = !(xs && xs[0] == '0');
     const char *ks = std::getenv("HALDA_KSLOT_SPLIT");  // parts of the k-slot scan split: 0 / 1 off, 2, 3
@@ -701,6 +895,7 @@ void halda_free(void *ctx) {
         if (x.ev) (void)hipEventDestroy(x.ev);
     }
     if (c->shard) (void)hipFree(c->shard);
+    if (c->emu) (void)hipFree(c->emu);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_host) (void)hipEventDestroy(c->ev_host);
     if (c->evf0) (void)hipEventDestroy(c->evf0);
@@ -830,12 +1025,13 @@ int halda_debug_dump(double *out) {
 }
 #endif
 
-int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
-                       int32_t n_k, halda_fleet_result *out, void *stream) {
-    Ctx *c = static_cast<Ctx *>(ctx);
-    if (!c || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL ctx/model/fleets/ks/out");
+}  // extern "C"
+
+namespace {
+// Argument checks shared by halda_solve_fleets and halda_fleets_plan_create (HALDA_OK: go on).
+int check_fleets_args(const halda_model *model, const halda_fleets *fleets, const int32_t *ks, int32_t n_k,
+                      const halda_fleet_result *out) {
     const halda_fleets &F = *fleets;
-    if (F.n_fleets <= 0) return HALDA_OK;
     if (n_k <= 0 || n_k > 1024) return fail(HALDA_E_ARG, "n_k must be in 1..1024");
     if (F.min_devices < 1 || F.max_devices < F.min_devices || F.max_devices > 4096)
         return fail(HALDA_E_ARG, "halda_fleets: need 1 <= min_devices <= max_devices <= 4096");
@@ -845,13 +1041,43 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
         return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
     if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
     if (model->L < 1) return fail(HALDA_E_ARG, "model.L < 1");
-    // ks (host memory): ascending, unique, positive; staged into the scratch below
+    // ks (host memory): ascending, unique, positive
+    for (int j = 0; j < n_k; ++j)
+        if (ks[j] < 1 || (j && ks[j] <= ks[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
+    return HALDA_OK;
+}
+
+// A prepared k-sweep (halda_fleets_plan_create): the fused sweep's plan, or, when the context runs
+// halda_solve_fleets another way (the CSR pipeline, more than 64 k), the call's arguments.
+struct FleetsPlan {
+    Ctx *c = nullptr;
+    bool fused = false;
+    SweepPlan p;
+    halda_model model;
+    halda_fleets F;
+    std::vector<int32_t> ks;
+    halda_fleet_result out;
+};
+}  // namespace
+
+extern "C" {
+
+int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                       int32_t n_k, halda_fleet_result *out, void *stream) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL ctx/model/fleets/ks/out");
+    const halda_fleets &F = *fleets;
+    if (F.n_fleets <= 0) return HALDA_OK;
+    {
+        const int rc = check_fleets_args(model, fleets, ks, n_k, out);
+        if (rc != HALDA_OK) return rc;
+    }
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     const int32_t *kh = ks;
-    for (int j = 0; j < n_k; ++j)
-        if (kh[j] < 1 || (j && kh[j] <= kh[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
-    if (c->fleets_fused && n_k <= 64) return sweep_fleets(c, *model, F, ks, n_k, *out, s);  // orders itself
+    // the fused sweep orders itself: per-stream scratch slots, and order_after_previous before a launch
+    // on the context's global tables
+    if (c->fleets_fused && n_k <= 64) return sweep_fleets(c, *model, F, ks, n_k, *out, s);
     {
         const int rc = order_after_previous(c, s);  // fleet_scratch / last_lowered are per context
         if (rc != HALDA_OK) return rc;
@@ -960,6 +1186,47 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
     c->have_lowered = true;
     return HALDA_OK;
 }
+
+int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                             int32_t n_k, const halda_fleet_result *out, void **plan) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !model || !fleets || !ks || !out || !plan) return fail(HALDA_E_ARG, "NULL ctx/model/fleets/ks/out/plan");
+    if (fleets->n_fleets > 0) {
+        const int rc = check_fleets_args(model, fleets, ks, n_k, out);
+        if (rc != HALDA_OK) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    FleetsPlan *P = new FleetsPlan();
+    P->c = c;
+    P->model = *model;
+    P->F = *fleets;
+    P->ks.assign(ks, ks + std::max(n_k, 0));
+    P->out = *out;
+    P->fused = fleets->n_fleets > 0 && c->fleets_fused && n_k <= 64;
+    if (P->fused) {
+        const int rc = plan_sweep(c, *model, *fleets, ks, n_k, *out, &P->p);
+        if (rc != HALDA_OK) {
+            delete P;
+            return rc;
+        }
+    }
+    *plan = P;
+    return HALDA_OK;
+}
+
+int halda_fleets_plan_launch(void *plan, void *stream) {
+    FleetsPlan *P = static_cast<FleetsPlan *>(plan);
+    if (!P) return fail(HALDA_E_ARG, "NULL plan");
+    if (P->F.n_fleets <= 0) return HALDA_OK;
+    Ctx *c = P->c;
+    if (!P->fused)
+        return halda_solve_fleets(c, &P->model, &P->F, P->ks.data(), int32_t(P->ks.size()), &P->out, stream);
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c->device) HIP_TRY(hipSetDevice(c->device));
+    return run_sweep(c, P->p, stream ? static_cast<hipStream_t>(stream) : c->stream);
+}
+
+void halda_fleets_plan_free(void *plan) { delete static_cast<FleetsPlan *>(plan); }
 
 // Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.
 constexpr size_t kZeroCopyBytes = size_t(1) << 20;
@@ -1233,78 +1500,107 @@ int halda_solve_fleets_sharded(void *ctx, void *comm, const halda_model *model, 
                                const int32_t *ks, int32_t n_k, halda_fleet_result *out, void *stream) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c || !comm || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL argument");
-    if (out->x || out->c) return fail(HALDA_E_ARG, "halda_solve_fleets_sharded: x / c are not gathered (pass NULL)");
-    if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
     ncclComm_t cm = static_cast<ncclComm_t>(comm);
     int world = 0, rank = 0;
     NCCL_TRY(ncclCommCount(cm, &world));
     NCCL_TRY(ncclCommUserRank(cm, &rank));
-    const halda_fleets &F = *fleets;
-    const int64_t nf = F.n_fleets;
-    if (nf <= 0) return HALDA_OK;
-    if (n_k <= 0 || n_k > 1024) return fail(HALDA_E_ARG, "n_k must be in 1..1024");
-    for (int j = 0; j < n_k; ++j)
-        if (ks[j] < 1 || (j && ks[j] <= ks[j - 1])) return fail(HALDA_E_ARG, "ks must be ascending, unique, > 0");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-    // this rank's k's: ks[rank], ks[rank + world], ... (halda_solve_distributed deals them the same way)
-    std::vector<int32_t> mine;
-    for (int j = rank; j < n_k; j += world) mine.push_back(ks[j]);
-    const int n_sub = int(mine.size());
-    // device count: nf * M for one fleet size, else read back from dev_off[nf] (a synchronous copy)
-    int64_t nd = nf * F.max_devices;
-    if (F.min_devices != F.max_devices) {
-        HIP_TRY(hipMemcpyAsync(&nd, F.dev_off + nf, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+    std::vector<ShardRank> R(1);
+    R[0].rank = rank;
+    R[0].o = *out;
+    // the ranks' all-reduces over RCCL, on this rank's results, in the step order of shard_steps
+    auto ar = [&](ShardField fld, size_t count) -> int {
+        const halda_fleet_result &o = R[0].o;
+        switch (fld) {
+            case kShObj: NCCL_TRY(ncclAllReduce(o.obj_value, o.obj_value, count, ncclFloat64, ncclMin, cm, s)); break;
+            case kShBestK: NCCL_TRY(ncclAllReduce(o.best_k, o.best_k, count, ncclInt32, ncclMin, cm, s)); break;
+            case kShGroupStart: NCCL_TRY(ncclGroupStart()); break;
+            case kShW: NCCL_TRY(ncclAllReduce(o.w, o.w, count, ncclInt32, ncclSum, cm, s)); break;
+            case kShN: NCCL_TRY(ncclAllReduce(o.n, o.n, count, ncclInt32, ncclSum, cm, s)); break;
+            case kShObk: NCCL_TRY(ncclAllReduce(o.obj_by_k, o.obj_by_k, count, ncclFloat64, ncclMin, cm, s)); break;
+            case kShSt: NCCL_TRY(ncclAllReduce(o.status, o.status, count, ncclInt32, ncclMax, cm, s)); break;
+            case kShGroupEnd: NCCL_TRY(ncclGroupEnd()); break;
+        }
+        return HALDA_OK;
+    };
+    return shard_steps(c, *model, *fleets, ks, n_k, world, R, s, ar);
+}
+
+int halda_solve_fleets_sharded_emulated(void *ctx, int32_t world, int32_t report_rank, const halda_model *model,
+                                        const halda_fleets *fleets, const int32_t *ks, int32_t n_k,
+                                        halda_fleet_result *out, void *stream) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !model || !fleets || !ks || !out) return fail(HALDA_E_ARG, "NULL argument");
+    if (world < 1 || world > kEmuMaxWorld || report_rank < 0 || report_rank >= world)
+        return fail(HALDA_E_ARG, "halda_solve_fleets_sharded_emulated: need 1 <= world <= 16, 0 <= report_rank < world");
+    if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
+    if (out->x || out->c) return fail(HALDA_E_ARG, "halda_solve_fleets_sharded: x / c are not gathered (pass NULL)");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    const int64_t nf = fleets->n_fleets;
+    if (nf <= 0) return HALDA_OK;
+    int64_t nd = 0;
+    {
+        const int rc = shard_device_count(*fleets, s, &nd);
+        if (rc != HALDA_OK) return rc;
     }
+    // every virtual rank but report_rank gets its own result arrays (the caller's are report_rank's)
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-    const size_t o_bk = take(4 * nf), o_obj = take(8 * nf), o_w = take(4 * size_t(nd)), o_n = take(4 * size_t(nd)),
-                 o_obk = take(8 * nf * std::max(n_sub, 1)), o_st = take(4 * nf * std::max(n_sub, 1));
-    if (off > c->shard_bytes) {
-        if (c->shard) HIP_TRY(hipFree(c->shard));
-        c->shard = nullptr;
-        c->shard_bytes = 0;
-        HIP_TRY(hipMalloc(&c->shard, off));
-        c->shard_bytes = off;
+    std::vector<size_t> o_bk(world), o_obj(world), o_w(world), o_n(world), o_obk(world), o_st(world);
+    for (int r = 0; r < world; ++r) {
+        o_bk[r] = take(4 * nf);
+        o_obj[r] = take(8 * nf);
+        o_w[r] = take(4 * size_t(nd));
+        o_n[r] = take(4 * size_t(nd));
+        o_obk[r] = take(8 * size_t(nf) * n_k);
+        o_st[r] = take(4 * size_t(nf) * n_k);
     }
-    char *base = static_cast<char *>(c->shard);
-    halda_fleet_result sub = {};
-    sub.best_k = reinterpret_cast<int32_t *>(base + o_bk);
-    sub.obj_value = reinterpret_cast<double *>(base + o_obj);
-    sub.w = reinterpret_cast<int32_t *>(base + o_w);
-    sub.n = reinterpret_cast<int32_t *>(base + o_n);
-    sub.obj_by_k = out->obj_by_k ? reinterpret_cast<double *>(base + o_obk) : nullptr;
-    sub.status = out->status ? reinterpret_cast<int32_t *>(base + o_st) : nullptr;
-    {
-        const int rc = order_after_previous(c, s);  // the shard scratch is per context
-        if (rc != HALDA_OK) return rc;
+    if (off > c->emu_bytes) {
+        if (c->emu) HIP_TRY(hipFree(c->emu));
+        c->emu = nullptr;
+        c->emu_bytes = 0;
+        HIP_TRY(hipMalloc(&c->emu, off));
+        c->emu_bytes = off;
     }
-    if (n_sub > 0) {
-        const int rc = halda_solve_fleets(ctx, model, fleets, mine.data(), n_sub, &sub, s);
-        if (rc != HALDA_OK) return rc;
+    char *base = static_cast<char *>(c->emu);
+    std::vector<ShardRank> R(static_cast<size_t>(world));
+    for (int r = 0; r < world; ++r) {
+        R[size_t(r)].rank = r;
+        halda_fleet_result &o = R[size_t(r)].o;
+        if (r == report_rank) {
+            o = *out;
+            continue;
+        }
+        o = {};
+        o.best_k = reinterpret_cast<int32_t *>(base + o_bk[r]);
+        o.obj_value = reinterpret_cast<double *>(base + o_obj[r]);
+        o.w = reinterpret_cast<int32_t *>(base + o_w[r]);
+        o.n = reinterpret_cast<int32_t *>(base + o_n[r]);
+        o.obj_by_k = out->obj_by_k ? reinterpret_cast<double *>(base + o_obk[r]) : nullptr;
+        o.status = out->status ? reinterpret_cast<int32_t *>(base + o_st[r]) : nullptr;
     }
-    const halda_fleet_result o = *out;
-    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 0, int(n_k), n_sub, rank, world,
-                       F.dev_off, sub, o);
-    HIP_TRY(hipGetLastError());
-    NCCL_TRY(ncclAllReduce(o.obj_value, o.obj_value, size_t(nf), ncclFloat64, ncclMin, cm, s));
-    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 1, int(n_k), n_sub, rank, world,
-                       F.dev_off, sub, o);
-    HIP_TRY(hipGetLastError());
-    NCCL_TRY(ncclAllReduce(o.best_k, o.best_k, size_t(nf), ncclInt32, ncclMin, cm, s));
-    hipLaunchKernelGGL(halda_shard_kernel, dim3(unsigned(nf)), dim3(64), 0, s, 2, int(n_k), n_sub, rank, world,
-                       F.dev_off, sub, o);
-    HIP_TRY(hipGetLastError());
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclAllReduce(o.w, o.w, size_t(nd), ncclInt32, ncclSum, cm, s));
-    NCCL_TRY(ncclAllReduce(o.n, o.n, size_t(nd), ncclInt32, ncclSum, cm, s));
-    if (o.obj_by_k) NCCL_TRY(ncclAllReduce(o.obj_by_k, o.obj_by_k, size_t(nf) * n_k, ncclFloat64, ncclMin, cm, s));
-    if (o.status) NCCL_TRY(ncclAllReduce(o.status, o.status, size_t(nf) * n_k, ncclInt32, ncclMax, cm, s));
-    NCCL_TRY(ncclGroupEnd());
-    hipLaunchKernelGGL(halda_shard_final_kernel, dim3(unsigned((nf + 255) / 256)), dim3(256), 0, s, int(nf), o);
-    HIP_TRY(hipGetLastError());
-    return HALDA_OK;
+    // each all-reduce as one device kernel over the virtual ranks' buffers (in place, every rank's copy
+    // gets the reduced value), in the step order of shard_steps
+    auto ar = [&](ShardField fld, size_t count) -> int {
+        if (fld == kShGroupStart || fld == kShGroupEnd) return HALDA_OK;
+        EmuReduce E = {};
+        E.world = world;
+        E.count = int64_t(count);
+        E.field = int(fld);
+        for (int r = 0; r < world; ++r) {
+            const halda_fleet_result &o = R[size_t(r)].o;
+            E.p[r] = fld == kShObj ? static_cast<void *>(o.obj_value) : fld == kShBestK ? static_cast<void *>(o.best_k)
+                   : fld == kShW ? static_cast<void *>(o.w) : fld == kShN ? static_cast<void *>(o.n)
+                   : fld == kShObk ? static_cast<void *>(o.obj_by_k) : static_cast<void *>(o.status);
+        }
+        if (count == 0) return HALDA_OK;
+        hipLaunchKernelGGL(halda_emu_allreduce_kernel, dim3(unsigned((count + 255) / 256)), dim3(256), 0, s, E);
+        HIP_TRY(hipGetLastError());
+        return HALDA_OK;
+    };
+    return shard_steps(c, *model, *fleets, ks, n_k, world, R, s, ar);
 }
 
 int halda_last_lowered(void *ctx, halda_batch *lowered, halda_result *solved) {

@@ -860,9 +860,8 @@ __device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
 // tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
 // only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
 // the one-fleet-per-wave table launch, as the register-only launch does.
-template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false>
-__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg, const DevFields &pre = {},
-                            int64_t pre_base = 0) {
+template <bool kTables, bool kGlobal, class SG = Wave>
+__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg) {
     constexpr int S = SG::S;
     constexpr bool kSeg = S < 64;
     constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
@@ -892,14 +891,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         // fleet size the loads are issued at once from dev_off[0] = 0 (the usual table) while the
         // scalar read of dev_off[0] is in flight, and reissued only where it is not 0: no dependent
         // round trip in front of the field loads.
-        // pre: the caller loaded this lane's fields already (the pipelined kernel, one fleet size, its
-        // dev_off[0] = pre_base applied)
-        DevFields mf;
-        if constexpr (kPre) mf = pre;
-        else mf = load_fields(F, d0 + (lane < M ? lane : 0));
-        if constexpr (kPre) {
-            d0 += pre_base;
-        } else if (A.uM > 0) {
+        DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
+        if (A.uM > 0) {
             // a vector read (returns in order behind the field loads: no wait of its own, unlike a
             // scalar read, whose lgkmcnt wait would also hold the kernel-argument reads)
             const int64_t base = __builtin_amdgcn_readfirstlane(int(F.dev_off[0])) |
@@ -1241,43 +1234,6 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
     sweep_fleet<false, false>(A, f, w, Wave(int(threadIdx.x & 63)));
-}
-
-// The register-only sweep, pipelined: a grid of nw waves (fewer than the fleets), wave w takes fleets
-// w, w + nw, w + 2 nw, ... and issues the field loads of its next fleet before it solves the current
-// one, so the next fleet's memory round trip hides behind this fleet's compute and the dispatcher
-// launches nw waves instead of one per fleet. One fleet size for the batch (uM <= 64), else the
-// one-fleet-per-wave kernel runs. The per-fleet work is sweep_fleet's, bit for bit.
-__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIMD) void halda_sweep_pipe_kernel(
-    SweepArgs A, int nw) {
-    const int wv = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
-    {
-        const int nf = A.F.n_fleets, nk = A.n_k, um = A.uM;
-        const int64_t *doff = A.F.dev_off;
-        const double bp = A.Mo.b_prime;
-        const double *tc = A.F.T_cpu;
-        const int32_t *ow = A.out.w;
-        asm volatile("" ::"s"(nf), "s"(nk), "s"(um), "s"(doff), "s"(bp), "s"(tc), "s"(ow));
-    }
-    const int nf = A.F.n_fleets;
-    if (wv >= nf) return;
-    const int lane = threadIdx.x & 63;
-    const int M = A.uM;
-    const int li = lane < M ? lane : 0;
-    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
-    WaveCtx w = {};
-    w.dparg = dparg[threadIdx.x >> 6];
-    // the first fleet's fields from dev_off[0] = 0 (the usual table), reloaded where it is not 0
-    DevFields nxt = load_fields(A.F, int64_t(wv) * M + li);
-    const int64_t base = __builtin_amdgcn_readfirstlane(int(A.F.dev_off[0])) |
-                         (int64_t(__builtin_amdgcn_readfirstlane(int(uint64_t(A.F.dev_off[0]) >> 32))) << 32);
-    if (base != 0) nxt = load_fields(A.F, base + int64_t(wv) * M + li);
-    for (int f = wv; f < nf; f += nw) {
-        const DevFields cur = nxt;
-        const int fn = f + nw;
-        if (fn < nf) nxt = load_fields(A.F, base + int64_t(fn) * M + li);  // in flight during this fleet
-        sweep_fleet<false, false, Wave, true>(A, f, w, Wave(lane), cur, base);
-    }
 }
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {

@@ -94,6 +94,19 @@ def _bind(lib):
                                                ctypes.POINTER(HaldaFleetsC), ctypes.c_void_p, ctypes.c_int32,
                                                ctypes.POINTER(HaldaFleetResultC), ctypes.c_void_p]
     lib.halda_solve_fleets_sharded.restype = ctypes.c_int
+    lib.halda_solve_fleets_sharded_emulated.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                        ctypes.POINTER(HaldaModelC), ctypes.POINTER(HaldaFleetsC),
+                                                        ctypes.c_void_p, ctypes.c_int32,
+                                                        ctypes.POINTER(HaldaFleetResultC), ctypes.c_void_p]
+    lib.halda_solve_fleets_sharded_emulated.restype = ctypes.c_int
+    lib.halda_fleets_plan_create.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaModelC), ctypes.POINTER(HaldaFleetsC),
+                                             ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(HaldaFleetResultC),
+                                             ctypes.POINTER(ctypes.c_void_p)]
+    lib.halda_fleets_plan_create.restype = ctypes.c_int
+    lib.halda_fleets_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.halda_fleets_plan_launch.restype = ctypes.c_int
+    lib.halda_fleets_plan_free.argtypes = [ctypes.c_void_p]
+    lib.halda_fleets_plan_free.restype = None
     lib._fleets_bound = True
     return lib
 
@@ -648,12 +661,52 @@ class DeviceFleetTable:
                                      o["n"].data_ptr(), o["obj_by_k"].data_ptr() if want_per_k else None,
                                      o["status"].data_ptr() if want_per_k else None, None, None)
         self.model = model_struct(model, kv_factor)
+        self._plans = {}
 
     def nbytes(self) -> int:
         return sum(int(t.numel() * t.element_size()) for t in self.arrs.values())
 
+    def plan(self, ctx):
+        """The prepared launch of this table on `ctx` (halda_fleets_plan_create: kernel choice, grids and
+        kernel arguments derived once), created on first use and kept with the table; set_fleets_path
+        on ctx afterwards needs replan()."""
+        p = self._plans.get(id(ctx))
+        if p is None:
+            lib = _bind(ctx.lib)
+            h = ctypes.c_void_p()
+            with ctx._lock:
+                rc = lib.halda_fleets_plan_create(ctx.ctx, ctypes.byref(self.model), ctypes.byref(self.fs),
+                                                  self.ks.ctypes.data, len(self.ks), ctypes.byref(self.res),
+                                                  ctypes.byref(h))
+            if rc != 0:
+                raise RuntimeError(f"halda_fleets_plan_create failed ({rc}): {last_error(lib)}")
+            p = (ctx, h, lib.halda_fleets_plan_launch)
+            self._plans[id(ctx)] = p
+        return p
+
+    def replan(self) -> None:
+        """Drop the prepared launches (after halda_set_fleets_path on their context)."""
+        for ctx, h, _ in self._plans.values():
+            _bind(ctx.lib).halda_fleets_plan_free(h)
+        self._plans.clear()
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.replan()
+        except Exception:
+            pass
+
     def launch(self, ctx, stream: int) -> None:
-        """Enqueue one k-sweep of every fleet on `stream` (a hipStream_t as int)."""
+        """Enqueue one k-sweep of every fleet on `stream` (a hipStream_t as int) through the prepared
+        plan: one ctypes call, one or two kernel enqueues."""
+        c, h, fn = self._plans.get(id(ctx)) or self.plan(ctx)
+        with ctx._lock:
+            rc = fn(h, stream)
+        if rc != 0:
+            raise RuntimeError(f"halda_fleets_plan_launch failed ({rc}): {last_error(ctx.lib)}")
+
+    def launch_unplanned(self, ctx, stream: int) -> None:
+        """The same k-sweep through halda_solve_fleets (shapes re-derived on every call)."""
         lib = _bind(ctx.lib)
         with ctx._lock:
             rc = lib.halda_solve_fleets(ctx.ctx, ctypes.byref(self.model), ctypes.byref(self.fs),
@@ -692,6 +745,19 @@ class RcclComm:
         if getattr(self, "comm", None):
             self.lib.halda_comm_destroy(self.comm)
             self.comm = None
+
+
+def launch_sharded_emulated(dt: "DeviceFleetTable", ctx, world: int, report_rank: int, stream: int) -> None:
+    """Latency mode's step sequence for `world` virtual ranks on this one GPU
+    (halda_solve_fleets_sharded_emulated): each RCCL all-reduce replaced, in order, by a device reduction
+    over the virtual ranks' arrays; virtual rank `report_rank`'s results land in dt.out."""
+    lib = _bind(ctx.lib)
+    with ctx._lock:
+        rc = lib.halda_solve_fleets_sharded_emulated(ctx.ctx, int(world), int(report_rank), ctypes.byref(dt.model),
+                                                     ctypes.byref(dt.fs), dt.ks.ctypes.data, len(dt.ks),
+                                                     ctypes.byref(dt.res), ctypes.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"halda_solve_fleets_sharded_emulated failed ({rc}): {last_error(lib)}")
 
 
 def launch_sharded(dt: "DeviceFleetTable", ctx, comm: RcclComm, stream: int) -> None:

@@ -203,6 +203,20 @@ typedef struct halda_fleet_result {
 int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                        int32_t n_k, halda_fleet_result *out, void *stream);
 
+/* A prepared halda_solve_fleets for a table that stays resident (a streaming deployment re-solves the
+ * same buffers as their contents change): the kernel choice, grids, LDS slices and kernel arguments are
+ * derived from the shapes once, at creation, so each halda_fleets_plan_launch() is one or two kernel
+ * enqueues on `stream` (NULL = the context's stream), asynchronous, with the results of a
+ * halda_solve_fleets call on the same arguments. The device arrays behind `fleets` / `out` must stay
+ * allocated with the same shapes (n_fleets, dev_off, min / max devices) while the plan lives; their
+ * contents may change between launches. The plan keeps the context's path (halda_set_fleets_path) as it
+ * was at creation. Launches of one context's plans must be serialised on the host, like every call on
+ * that context. */
+int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
+                             int32_t n_k, const halda_fleet_result *out, void **plan);
+int halda_fleets_plan_launch(void *plan, void *stream);
+void halda_fleets_plan_free(void *plan);
+
 /* How halda_solve_fleets runs (default 1; HALDA_FLEETS_PATH=csr / =wave at halda_init select 0 / 2):
  * 1 the fused sweep (halda_sweep_kernel: every (fleet, k) built in registers from the device
  *   fields, solved and compared in one wave per fleet; no MILP is materialised); batches of more
@@ -259,6 +273,16 @@ int halda_comm_init(void **comm, int world, int rank, const void *id128, int dev
 void halda_comm_destroy(void *comm);
 int halda_solve_fleets_sharded(void *ctx, void *comm, const halda_model *model, const halda_fleets *fleets,
                                const int32_t *ks, int32_t n_k, halda_fleet_result *out, void *stream);
+
+/* Latency mode's exact step sequence for `world` virtual ranks (1..16) on ONE device, for tests and
+ * measurement where a node's GPUs are not available: every virtual rank's sub-sweep and shard kernels run
+ * into its own result arrays (library scratch), and each RCCL all-reduce of halda_solve_fleets_sharded is
+ * replaced, in the same order, by one device kernel reducing over the virtual ranks' arrays (MIN / SUM /
+ * MAX as there). The arrays of virtual rank `report_rank` are the caller's `out`. Asynchronous on
+ * `stream`. */
+int halda_solve_fleets_sharded_emulated(void *ctx, int32_t world, int32_t report_rank, const halda_model *model,
+                                        const halda_fleets *fleets, const int32_t *ks, int32_t n_k,
+                                        halda_fleet_result *out, void *stream);
 
 /* The lowered batch of the last halda_solve_fleets call (device pointers into ctx
  * scratch, valid until the next call on ctx): for tests and diagnostics. An

@@ -90,3 +90,39 @@ def test_rccl_sharded_latency_mode_world_one():
             assert (b.out["best_k"] > 0).all()
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8, 10])
+def test_sharded_latency_mode_emulated_ranks(world):
+    """The C ABI's latency mode at world > 1 on one GPU (halda_solve_fleets_sharded_emulated): `world`
+    virtual ranks each sweep ks[r], ks[r + world], ... into their own arrays, and each RCCL all-reduce of
+    halda_solve_fleets_sharded is a device reduction over the ranks' arrays, in the same order -- so the
+    k dealing, the owner / tie kernel modes 1 and 2 and (world 10 > 9 k) a rank with no k at all all run.
+    Every virtual rank ends with exactly the single-GPU sweep's results (best k, obj_value, w, n,
+    obj_by_k, status; halda_p_solver.py:407's tie rule) on a C2 batch and a ragged batch."""
+    import torch
+
+    from distilp_amd.common import DeviceProfile, ModelProfileSplit
+    from distilp_amd.solver._libhalda import get_context
+    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table, launch_sharded_emulated
+    from distilp_amd.synth import load_model_dict, synth_fleet
+
+    m2 = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    stream = torch.cuda.Stream(dev)
+    for sizes in ([16] * 100, [1 + (s * 5) % 64 for s in range(80)]):
+        fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(3300 + s, M)] for s, M in enumerate(sizes)]
+        table = fleet_table(fleets, m2)
+        a = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+        a.launch(ctx, stream.cuda_stream)
+        for rank in sorted({0, world - 1, world // 2}):
+            b = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+            for t in b.out.values():
+                t.fill_(-7)
+            launch_sharded_emulated(b, ctx, world, rank, stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status"):
+                assert torch.equal(a.out[f], b.out[f]), (world, rank, f)
+        assert (a.out["best_k"] > 0).all()

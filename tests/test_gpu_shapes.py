@@ -96,3 +96,41 @@ def test_wide_fleet_and_big_tables(llama_online_model):
     for devs, r in zip(fleets, got):
         want, _ = mo.halda_solve_oracle(devs, model, k_candidates=[1, 2, 4], kv_bits="4bit", solver="exact")
         assert r.k == want["k"] and _close(r.obj_value, want["obj_value"]), (len(devs), r, want)
+
+
+def test_big_table_launches_on_two_streams(llama_online_model):
+    """Batches whose tables exceed the LDS budget share the context's global-memory tables
+    (halda_sweep_big_kernel / halda_solve_big_kernel): two such fused-sweep batches alternating over two
+    streams, with a CSR-pipeline batch on global tables in between, must each give the results of one
+    synchronous call, bit for bit (the big launches are ordered after the previous one on another
+    stream; without that they would write the same table slices concurrently)."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table, solve_table
+
+    model = llama_online_model.model_copy(update={"L": 256})
+    ks = [1, 2, 4]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    tables = [fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(s, M)]
+                           for s, M in zip(range(b * 8, b * 8 + 8), (100, 80, 72, 96, 66, 100, 90, 70))], model)
+              for b in range(2)]
+    want = [solve_table(t, model, ks, 0.5, want_x=False) for t in tables]
+    dts = [DeviceFleetTable(t, model, ks, 0.5, dev, want_per_k=True) for t in tables]
+    mid_fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(s, 100)] for s in (40, 41)]
+    lowered = [lower_fleet(devs, model, "4bit") for devs in mid_fleets]
+    batch, _ = assemble(lowered, [ks] * len(lowered))
+    mid_want = ctx.solve(batch)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    for i in range(6):
+        dts[i % 2].launch(ctx, streams[i % 2].cuda_stream)
+        if i == 3:
+            mid = ctx.solve(batch)
+            assert np.array_equal(mid.status, mid_want.status) and np.array_equal(mid.x, mid_want.x)
+    torch.cuda.synchronize(dev)
+    for d, w in zip(dts, want):
+        assert np.array_equal(d.out["best_k"].cpu().numpy(), w.best_k)
+        assert np.array_equal(d.out["w"].cpu().numpy(), w.w) and np.array_equal(d.out["n"].cpu().numpy(), w.n)
+        assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)
+        assert np.array_equal(d.out["status"].cpu().numpy(), w.status.ravel())
+        assert np.array_equal(d.out["obj_by_k"].cpu().numpy(), w.obj_by_k.ravel())

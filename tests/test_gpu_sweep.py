@@ -309,3 +309,42 @@ def test_uniform_fleets_viewed_from_an_offset_dev_off(llama_online_model, M):
     d0 = skip * M
     assert np.array_equal(got["w"][d0:], full["w"][d0:]) and np.array_equal(got["n"][d0:], full["n"][d0:])
     assert (got["w"][:d0] == -1).all()  # devices of the fleets outside the view are untouched
+
+
+@pytest.mark.parametrize("sizes", [[64] * 100, [16] * 100, [5, 16, 9] * 30, [3] * 10, [70, 40] * 3])
+def test_prepared_plan_equals_solve_fleets(llama_online_model, sizes):
+    """halda_fleets_plan_create / _launch (the bench's and a streaming caller's launch) against
+    halda_solve_fleets on the same resident buffers: register, k-slot, table-alone and wide (gated table)
+    launch sequences give the same bits; the plan reads the buffers' CURRENT contents, so a table
+    rewritten in place between launches (a re-profiled fleet stream, config C5) is solved as rewritten."""
+    import torch
+
+    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, DeviceFleetTable
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(23000 + s, M)] for s, M in enumerate(sizes)]
+    table = fleet_table(fleets, llama_online_model)
+    want = solve_table(table, llama_online_model, ks, 0.5)
+    dt = DeviceFleetTable(table, llama_online_model, ks, 0.5, dev, want_per_k=True)
+    stream = torch.cuda.Stream(dev)
+    for _ in range(2):
+        dt.launch(ctx, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(dt.out["best_k"].cpu().numpy(), want.best_k)
+        assert np.array_equal(dt.out["obj_value"].cpu().numpy(), want.obj_value)
+        assert np.array_equal(dt.out["w"].cpu().numpy(), want.w) and np.array_equal(dt.out["n"].cpu().numpy(), want.n)
+        assert np.array_equal(dt.out["status"].cpu().numpy(), want.status.ravel())
+        assert np.array_equal(dt.out["obj_by_k"].cpu().numpy(), want.obj_by_k.ravel())
+    rng = np.random.default_rng(5)
+    moved = table.perturbed(rng)
+    for f in F64_FIELDS + I64_FIELDS:  # rewrite the resident table in place
+        dt.arrs[f].copy_(torch.from_numpy(np.ascontiguousarray(getattr(moved, f))))
+    want2 = solve_table(moved, llama_online_model, ks, 0.5)
+    dt.launch(ctx, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert np.array_equal(dt.out["best_k"].cpu().numpy(), want2.best_k)
+    assert np.array_equal(dt.out["obj_value"].cpu().numpy(), want2.obj_value)
+    assert np.array_equal(dt.out["w"].cpu().numpy(), want2.w)
+    dt.replan()

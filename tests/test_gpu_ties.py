@@ -1,0 +1,111 @@
+"""GPU parity on fleets of repeated devices: exact ties between devices' increments and cycle times.
+
+The k-slot kernel splits the k = 2 threshold scan over two waves (ScanSplit, halda_solve.hpp); the
+helper wave starts from the greedy's optimal capped allocation at the cut, which under ties need not be
+the allocation the one scan holds there (tests/test_scan_split_model.py states why the result is still
+exact). These fleets make such ties certain: the reference's own "same device twice" fleet
+(test/test_integration.py:88) and homogeneous / half-duplicated 16-device fleets (tests/ties.py), in
+batches of more than 64 fleets, so halda_solve_fleets takes the default k-slot kernel. Per (fleet, k)
+against the exact oracle (status; c.x and the objective within 1e-9; (w, n) where the optimum is
+unique), the best k against the oracle's sweep (ascending k, strict <, halda_p_solver.py:391-412), and
+the unsplit (path 5) / two-part (default) / three-part (path 6) scans against each other."""
+
+import contextlib
+import io
+
+import numpy as np
+import pytest
+
+from distilp_amd.solver._libhalda import STATUS_INFEASIBLE, STATUS_OPTIMAL, get_context
+from distilp_amd.solver.coefficients import valid_factors_of_L
+from distilp_amd.solver.fleets import fleet_table, solve_table
+from oracle import milp_oracle as mo
+
+from .ties import FIXTURE_FOLDERS, fixture_twice, tied_fleets
+
+pytestmark = pytest.mark.gpu
+
+OBJ_REL = 1e-9
+
+
+def _close(a, b, rel=OBJ_REL):
+    return abs(a - b) <= rel * max(1.0, abs(b))
+
+
+def _ks(model):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return sorted(valid_factors_of_L(model.L))
+
+
+@pytest.mark.parametrize("folder", FIXTURE_FOLDERS)
+def test_kslot_split_scan_on_tied_fleets(folder):
+    twice, model = fixture_twice(folder)
+    fleets = [twice] + [devs for _, devs in tied_fleets(24)]
+    assert len(fleets) > 64 and max(len(f) for f in fleets) <= 16
+    ks = _ks(model)
+    table = fleet_table(fleets, model)
+    ctx = get_context(0)
+    runs = {}
+    try:
+        for path in ("fused", "kslot_unsplit", "kslot_split3"):
+            ctx.set_fleets_path(path)
+            ctx.set_timing(True)
+            runs[path] = solve_table(table, model, ks, 0.5, want_x=True)
+            assert "halda_sweep_kslot_kernel" in ctx.last_fleet_ms(), path
+    finally:
+        ctx.set_fleets_path("fused")
+        ctx.set_timing(False)
+    res = runs["fused"]
+    n_open = n_unique = 0
+    for f, devs in enumerate(fleets):
+        M = len(devs)
+        best = None
+        for j, k in enumerate(ks):
+            p = mo.lower_dense(devs, model, k, 0.5)
+            st, xo, b1, b2, _ = mo.exact_solve(p)
+            if st == 2:
+                assert res.status[f, j] == STATUS_INFEASIBLE, (f, k)
+                continue
+            assert res.status[f, j] == STATUS_OPTIMAL, (f, k, res.status[f, j])
+            n_open += 1
+            x = res.x[f, j, :p["c"].shape[0]]
+            assert _close(float(np.dot(p["c"], x)), b1), (f, k, float(np.dot(p["c"], x)), b1)
+            obj = mo.objective_value(p, x)
+            assert _close(float(res.obj_by_k[f, j]), obj), (f, k)
+            if mo.uniqueness_margin_ok(b1, b2):
+                n_unique += 1
+                assert np.array_equal(x[:2 * M], xo[:2 * M]), (f, k)
+            if best is None or obj < best[0]:
+                best = (obj, k)
+        assert best is not None and res.best_k[f] == best[1], (f, res.best_k[f], best)
+        a, b = table.dev_off[f], table.dev_off[f + 1]
+        assert int(res.w[a:b].sum()) * int(res.best_k[f]) == model.L  # test_integration.py:112
+    assert n_open >= len(fleets)
+    # the three scan layouts: the same statuses and best k, the same objectives (allocations may differ
+    # only where the optimum is not unique, and then by rounding of the same optimum)
+    for path in ("kslot_unsplit", "kslot_split3"):
+        other = runs[path]
+        assert np.array_equal(other.status, res.status), path
+        assert np.array_equal(other.best_k, res.best_k), path
+        fin = res.status == STATUS_OPTIMAL
+        assert np.allclose(other.obj_by_k[fin], res.obj_by_k[fin], rtol=1e-12, atol=0.0), path
+        assert np.allclose(other.obj_value, res.obj_value, rtol=1e-12, atol=0.0), path
+
+
+@pytest.mark.parametrize("folder", FIXTURE_FOLDERS)
+def test_halda_solve_same_device_twice(folder):
+    """test_integration.py:88-112 through the unchanged API: one fixture device twice, kv 4bit,
+    mip_gap 1e-4 -- k, obj_value and sum(w) * k == L against the reference's arithmetic (the oracle's
+    HiGHS path), (w, n) against it where the exact oracle finds the optimum unique."""
+    from distilp_amd.solver import halda_solve
+
+    devs, model = fixture_twice(folder)
+    with contextlib.redirect_stdout(io.StringIO()):
+        r = halda_solve(devs, model, mip_gap=1e-4, plot=False, kv_bits="4bit")
+    want, per_k = mo.halda_solve_oracle(devs, model, mip_gap=1e-4, kv_bits="4bit", solver="highs")
+    assert r.k == want["k"] and r.k > 0 and len(r.w) == 2 and sum(r.w) * r.k == model.L
+    assert _close(r.obj_value, want["obj_value"]), (r.obj_value, want["obj_value"])
+    ex, ex_k = mo.halda_solve_oracle(devs, model, mip_gap=1e-4, kv_bits="4bit", solver="exact")
+    rec = next(q for q in ex_k if q["k"] == ex["k"])
+    if rec["margin"] > 1e-7 * max(1.0, abs(rec["obj_value"])):
+        assert (r.w, r.n) == (ex["w"], ex["n"])

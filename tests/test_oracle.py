@@ -88,3 +88,23 @@ def test_golden_files_are_data_only():
     """Goldens hold inputs/outputs only (no reference source text)."""
     for p in GOLDEN.glob("*.json"):
         json.loads(p.read_text())
+
+
+def test_exact_oracle_matches_highs_on_tied_fleets(llama_online_model):
+    """Fleets of repeated devices (tests/ties.py; the reference's own "same device twice",
+    test/test_integration.py:88): the exact C solver and the reference's arithmetic (dense lowering +
+    scipy HiGHS) agree on status and objective per k, so the GPU tie test (test_gpu_ties.py) checks
+    against a pinned oracle there too. Ties make the optimum non-unique, so (w, n) is not compared."""
+    from .ties import FIXTURE_FOLDERS, fixture_twice, tied_fleets
+
+    cases = [fixture_twice(f) for f in FIXTURE_FOLDERS]
+    cases += [(devs, llama_online_model) for _, devs in tied_fleets(2)]
+    for devs, model in cases:
+        hi, hk = mo.halda_solve_oracle(devs, model, kv_bits="4bit", solver="highs")
+        ex, ek = mo.halda_solve_oracle(devs, model, kv_bits="4bit", solver="exact")
+        assert hi["k"] == ex["k"]
+        assert abs(hi["obj_value"] - ex["obj_value"]) <= 1e-9 * max(1.0, abs(ex["obj_value"]))
+        for a, b in zip(hk, ek):
+            assert a["k"] == b["k"] and a["success"] == b["success"]
+            if a["success"]:
+                assert abs(a["obj_value"] - b["obj_value"]) <= 1e-9 * max(1.0, abs(b["obj_value"]))

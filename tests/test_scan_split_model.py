@@ -42,3 +42,55 @@ def test_split_parts_merge_to_the_one_scan(seed):
     for f in range(len(Gs)):  # the one scan is the brute-force optimum
         r = sm.model(G[f], H[f], 1.0, 0)
         assert abs(r["best"] - r["brute"]) <= 1e-9 * max(1.0, abs(r["brute"]))
+
+
+def _tied_tables(rng, M, R1, kind):
+    """Tables with exact ties, as fleets of repeated devices produce them (the reference's own "same
+    device twice", test/test_integration.py:88, and homogeneous clusters): `kind` "copies" -- every row
+    one device's; "two" -- two devices, each M / 2 times; "half" -- half the rows duplicates of the
+    other half; "grid" -- distinct rows whose increments and cycle times come from a coarse grid
+    (ties across different devices)."""
+    def row(grid=False):
+        if grid:
+            inc = np.sort(rng.integers(1, 4, R1 - 1).astype(float)) / 4
+            h = 0.25 + np.cumsum(rng.integers(0, 2, R1).astype(float)) / 8
+        else:
+            inc = np.sort(rng.uniform(0.01, 1.0, R1 - 1))
+            h = rng.uniform(0.05, 0.3) + np.cumsum(rng.uniform(0.0, 0.1, R1))
+        return np.concatenate([[0.0], np.cumsum(inc)]) + (0.0 if grid else rng.uniform(0.0, 1.0)), h
+
+    if kind == "copies":
+        rows = [row()] * M
+    elif kind == "two":
+        a, b = row(), row()
+        rows = [a] * (M // 2) + [b] * (M - M // 2)
+    elif kind == "half":
+        base = [row() for _ in range(M // 2)]
+        rows = base + base[: M - M // 2]
+    else:
+        rows = [row(grid=True) for _ in range(M)]
+    return np.array([r[0] for r in rows]), np.array([r[1] for r in rows])
+
+
+@pytest.mark.parametrize("kind", ["copies", "two", "half", "grid"])
+@pytest.mark.parametrize("M", [2, 16])
+def test_split_parts_exact_under_increment_ties(kind, M):
+    """The helper parts start from the greedy's optimal capped allocation at their cut, which under ties
+    need not be the allocation the one scan holds there. The exchange step keeps ANY optimal capped
+    allocation optimal (its largest taken increment lam and the set of useful openings are the same for
+    every optimal allocation), so the merged optimum must still be the brute-force one."""
+    rng = np.random.default_rng(1000 + M)
+    R1 = 2 * M + 6
+    Gs, Hs = [], []
+    for _ in range(16):
+        g, h = _tied_tables(rng, M, R1, kind)
+        Gs.append(g)
+        Hs.append(h)
+    G, H = np.array(Gs), np.array(Hs)
+    for kc in (0.5, 1.0, 4.0):
+        rep = sm.split_report(G, H, len(Gs), kc=kc)
+        for parts, (_, _, agree) in rep.items():
+            assert agree, (parts, kc)
+        for f in range(len(Gs)):
+            r = sm.model(G[f], H[f], kc, 0)
+            assert abs(r["best"] - r["brute"]) <= 1e-9 * max(1.0, abs(r["brute"])), (f, kc)
