@@ -118,7 +118,7 @@ def algorithmic_bytes(lowered, refs, n_k: int):
     W < M (the screen settles it) the w bounds, the C column and the equality-row bounds; pick: per
     instance its status, per optimal instance its header, c and x, per fleet the offsets in and best k,
     obj_value and w / n out, obj_by_k / status when requested (not in the bench)."""
-    solve = screen = fused = lower = pick = 0
+    solve = screen = lower = pick = 0
     fleets_seen, fleets_solved = set(), set()
     for ref in refs:
         fl = lowered[ref.fleet]
@@ -136,21 +136,18 @@ def algorithmic_bytes(lowered, refs, n_k: int):
             if ref.fleet not in fleets_solved:  # a solved fleet's CSR is read once per launch
                 fleets_solved.add(ref.fleet)
                 solve += csr
-                fused += csr
             one = HDR + 25 * nc + 16 * nr + 8 * nc + RES
             solve += one
-            fused += one + 1
             lower += 25 * nc + 16 * nr
             pick += HDR + 16 * nc
         else:
             screen += RES
-            fused += scr + RES
             lower += 16 * M + 25 + 16
     # fused k-sweep (no CSR): device fields in, per fleet best k / obj_value / w / n out -- the first
     # launch (register or lane-segment kernel), or the table kernel when it runs the whole batch alone
     # (as the dominant launch it does; as the gated second launch it only redoes flagged fleets)
     sweep = sum(DEV_FIELDS * fl.M + 8 + 4 + 8 + 8 * fl.M for fl in lowered)
-    return {"halda_screen_k1_kernel": fused, "halda_screen_kernel": screen, "halda_solve_k1_kernel": solve,
+    return {"halda_screen_kernel": screen, "halda_solve_k1_kernel": solve,
             "halda_lower_kernel": lower, "halda_pick_kernel": pick, "halda_sweep_kernel": sweep,
             "halda_sweep_seg_kernel": sweep, "halda_sweep_tables_kernel": sweep}
 
@@ -357,11 +354,15 @@ def timed_events(step, steps, torch, dev, stream):
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), or None when none covers this kernel."""
-    cands = sorted((REPO / "profiles").glob("r*_pmc.json"))
-    for c in reversed(cands):
+    (profiles/*_pmc.json, written by tools/pmc_summary.py) recorded for THIS libhalda.so build (its
+    libhalda_sha256), or None when none covers this kernel and build."""
+    sha = lib_sha256()
+    for c in sorted((REPO / "profiles").glob("r*_pmc.json"), reverse=True):
         try:
-            return json.loads(c.read_text())["kernels"][kernel]["hbm_bytes_per_launch"]
+            j = json.loads(c.read_text())
+            if j.get("libhalda_sha256") != sha:
+                continue
+            return j["kernels"][kernel]["hbm_bytes_per_launch"]
         except Exception:  # noqa: BLE001
             continue
     return None

@@ -76,8 +76,11 @@ static int rate(PyObject *table, PyObject *Q, int fq, int *present, double *v) {
 /* ---------------------------------------------------------------- fast (parallel) pass
  * Large tables are packed by several threads while the calling thread holds the GIL and waits (small
  * ones by the calling thread itself), so
- * no Python code runs and no object changes meanwhile. The workers only READ: borrowed instance
- * dicts (_PyObject_GetDictPtr), lookups by precomputed hash in str-keyed dicts
+ * no Python code runs and no object changes meanwhile. The calling thread first collects every
+ * device's instance dict (_PyObject_GetDictPtr, which on CPython 3.11+ may create the dict of an
+ * object whose attributes are still inline: that happens there, under the GIL, never in a worker; an
+ * object without an exact str-keyed dict sends the table to the serial pass). The workers only READ:
+ * those borrowed dicts, lookups by precomputed hash in str-keyed dicts
  * (_PyDict_GetItem_KnownHash: no error state, no Python code), and the values of exact float / int /
  * bool / None / str / dict objects. No reference count changes, no allocation, no exception: any
  * value outside that (a missing key, another type, an overflow, a FLOPs table without "b_1") makes the
@@ -85,7 +88,7 @@ static int rate(PyObject *table, PyObject *Q, int fq, int *present, double *v) {
  * reference's exceptions in the reference's order. So the parallel pass either writes exactly what
  * the serial one would, or nothing that is kept. */
 typedef struct {
-    PyObject **devs;
+    PyObject **devs; /* the devices' instance dicts */
     Py_ssize_t lo, hi, nd;
     PyObject *Q;
     Py_hash_t hQ;
@@ -132,11 +135,9 @@ static int fthru(PyObject *o) {
     return PyFloat_AS_DOUBLE(o) != 0.0;
 }
 
-/* one device, the serial pass's reads restricted to the plain cases; -1: give up */
-static int fast_dev(const Job *J, PyObject *obj, Py_ssize_t g) {
-    PyObject **dp = _PyObject_GetDictPtr(obj);
-    if (!dp || !fdict(*dp)) return -1;
-    PyObject *d = *dp, *o;
+/* one device (its instance dict d), the serial pass's reads restricted to the plain cases; -1: give up */
+static int fast_dev(const Job *J, PyObject *d, Py_ssize_t g) {
+    PyObject *o;
     PyObject *os = FGET(d, os_type);
     if (!os || !PyUnicode_CheckExact(os)) return -1;
     int c = 3;
@@ -222,24 +223,16 @@ static int fast_dev(const Job *J, PyObject *obj, Py_ssize_t g) {
  * PF_NEAR devices ahead the dict's entries and every value object they point at. Reads only. */
 enum { PF_FAR = 8, PF_NEAR = 3 };
 
-static void prefetch_obj(PyObject *obj) {
-    __builtin_prefetch(obj);
-    PyObject **dp = _PyObject_GetDictPtr(obj);
-    if (dp && *dp) __builtin_prefetch(*dp);
-}
-
-static void prefetch_values(PyObject *obj) {
-    PyObject **dp = _PyObject_GetDictPtr(obj);
-    if (!dp || !*dp || !PyDict_CheckExact(*dp)) return;
+static void prefetch_values(PyObject *d) {
     Py_ssize_t pos = 0;
     PyObject *k, *v;
-    while (PyDict_Next(*dp, &pos, &k, &v)) __builtin_prefetch(v);
+    while (PyDict_Next(d, &pos, &k, &v)) __builtin_prefetch(v);
 }
 
 static void *worker(void *arg) {
     const Job *J = (const Job *)arg;
     for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g) {
-        if (g + PF_FAR < J->hi) prefetch_obj(J->devs[g + PF_FAR]);
+        if (g + PF_FAR < J->hi) __builtin_prefetch(J->devs[g + PF_FAR]);
         if (g + PF_NEAR < J->hi) prefetch_values(J->devs[g + PF_NEAR]);
         if (fast_dev(J, J->devs[g], g)) *J->bail = 1;
     }
@@ -275,7 +268,12 @@ static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f
         const Py_ssize_t M = PySequence_Fast_GET_SIZE(fl);
         if (M == 0 || g + M > nd) { free(devs); return 0; }
         PyObject **items = PySequence_Fast_ITEMS(fl);
-        for (Py_ssize_t i = 0; i < M; ++i) devs[g + i] = items[i];
+        for (Py_ssize_t i = 0; i < M; ++i) {
+            if (i + PF_FAR < M) __builtin_prefetch(items[i + PF_FAR]);
+            PyObject **dp = _PyObject_GetDictPtr(items[i]); /* under the GIL: may create the dict (3.11+) */
+            if (!dp || !*dp || !fdict(*dp)) { free(devs); return 0; }
+            devs[g + i] = *dp;
+        }
         g += M;
         off[f + 1] = g;
     }

@@ -56,8 +56,6 @@ struct Ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evk = nullptr;  // start, end, after k = 1, after screen
     bool timed = false;
     bool timing = true;  // record the per-launch HIP events (halda_set_timing)
-    bool two_pass = true;  // HALDA_TWO_PASS=0: the fused one-wave-per-instance screen + k = 1 kernel
-    bool xcd_swizzle = true;  // HALDA_XCD_SWIZZLE=0: block b works on instance b
     int *hb_flag = nullptr;  // launch id of the last launch with a k = 1 hand-back
     int launch_id = 0;
     void *scratch = nullptr;  // host-API staging (device)
@@ -285,16 +283,8 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     const int launch_id = ++ctx->launch_id;  // tags this launch's k = 1 hand-backs (no reset needed)
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
-    if (!ctx->two_pass) {
-        // one wave per instance: screen, then the k = 1 solve for the survivors
-        int per_cu = 0;
-        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_screen_k1_kernel), lds1, &per_cu));
-        hipLaunchKernelGGL(halda_screen_k1_kernel, dim3(unsigned(in.n_inst)), dim3(64), size_t(lds1), stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc), hb_flag, launch_id, int(ctx->xcd_swizzle));
-        HIP_TRY(hipGetLastError());
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
-    } else {
-        // two passes: screen kernel (8 instances per wave), then a persistent k = 1 kernel
+    {
+        // screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
                            cls, mmax, in.max_R1, int(tab), int(tab_kc));
@@ -852,13 +842,9 @@ int halda_init(int device_ordinal, void **ctx_out) {
         delete c;
         return fail(HALDA_E_HIP, "hand-back flag allocation failed");
     }
-    const char *tp = std::getenv("HALDA_TWO_PASS");
-    c->two_pass = !(tp && tp[0] == '0');
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
-    const char *xs = std::getenv("HALDA_XCD_SWIZZLE");
-    c->xcd_swizzle = !(xs && xs[0] == '0');
     const char *ks = std::getenv("HALDA_KSLOT_SPLIT");  // parts of the k-slot scan split: 0 / 1 off, 2, 3
     c->kslot_split = ks ? std::max(0, std::min(std::atoi(ks), kMaxSplitParts)) : 2;
     c->kslot_split_env = c->kslot_split;

@@ -27,12 +27,6 @@ __device__ double g_halda_dump[kDumpFleets * kDumpDev * kDumpE * 2];
     do {                                                                                                \
         if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-// slots 7..9 of the fused kernel's waves: shader clock at wave start, constant-rate
-// (100 MHz) clock at wave start and at wave end
-#define HALDA_WSTAMP(slot, v)                                                                           \
-    do {                                                                                                \
-        if (lane == 0 && inst < kStampInst) g_halda_stamps[inst * kStamps + (slot)] = (v);              \
-    } while (0)
 // fused sweep: per-fleet stamps (slot 0..6 shader clock, 7/8 constant-rate clock at start / end);
 // with -DHALDA_STAMPS_DP per-instance stamps of the table path instead (HALDA_TSTAMP, slots 0, 6-8)
 #ifdef HALDA_STAMPS_DP
@@ -59,16 +53,12 @@ __device__ double g_halda_dump[kDumpFleets * kDumpDev * kDumpE * 2];
 #elif defined(HALDA_MARKS)  // asm listing only: phase markers for tools/asm_regions.py
 #define HALDA_SSTAMP(slot, v) asm volatile("; PHASE_MARK " #slot)
 #define HALDA_TSTAMP(slot) do {} while (0)
-#define HALDA_WSTAMP(slot, v) do {} while (0)
 #define HALDA_STAMP(k) do {} while (0)
 #else
 #define HALDA_SSTAMP(slot, v) \
     do {                      \
     } while (0)
 #define HALDA_TSTAMP(slot) do {} while (0)
-#define HALDA_WSTAMP(slot, v) \
-    do {                      \
-    } while (0)
 #define HALDA_STAMP(k) \
     do {               \
     } while (0)

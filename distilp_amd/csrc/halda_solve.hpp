@@ -2106,130 +2106,3 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
         }
     }
 }
-
-// Screen of ONE instance by one wave (lane = device): the same verdicts as
-// screen_group (neither reads the w upper bounds: a device whose w range is
-// empty makes the solve report the instance infeasible). Returns the class; settles (and writes) everything but CLS_K1 /
-// CLS_GEN. Uniform header values are returned for the solve.
-struct Head {
-    int N, m, M;
-    int64_t co, ro, cs;
-    double Wd, kc;
-};
-
-__device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t inst, int lane,
-                                 int mmax, int r1max, int tab, int tab_kc, Head &h) {
-    h.N = B.n_cols[inst];
-    h.m = B.n_rows[inst];
-    h.co = B.col_off[inst];
-    h.ro = B.row_off[inst];
-    h.cs = B.csr_off[inst];
-    int status = 0;
-    if (h.N < 1 || (h.N - 1) % 7 != 0 || h.m < 1) status = HALDA_STATUS_UNSUPPORTED;
-    h.M = status ? 0 : (h.N - 1) / 7;
-    if (!status && h.M > mmax) status = HALDA_STATUS_TOO_LARGE;
-    const int M = h.M, ma = max(h.m, 1);
-    // round trip 2 (branch-free): equality-row extent and bounds, c[C], this lane's w bounds
-    const int32_t *rp = B.row_ptr + h.cs;
-    const int eqs = rp[ma - 1], eqe = rp[ma];
-    const double Wd = B.row_ub[h.ro + ma - 1], Wl = B.row_lb[h.ro + ma - 1];
-    const double cC = B.c[h.co + 7 * int64_t(M)];
-    const int li = lane < M ? lane : 0;
-    const double lb = B.col_lb[h.co + li];  // w upper bounds are left to the solve (decode / tables)
-    h.Wd = Wd;
-    h.kc = cC;
-    if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
-        status = HALDA_STATUS_UNSUPPORTED;
-    int verdict = CLS_DONE;
-    if (!status) {
-        // round trip 3: the equality row (lane = device)
-        const int c0 = B.col_idx[eqs + li];
-        const double v0 = B.val[eqs + li];
-        int bad = 0, infeas = 0, sumlo = 0;
-        auto one = [&](int i, int col, double v, double l) {
-            bad |= col != i || v != 1.0;
-            const int wlo = int(ceil(l));
-            infeas |= wlo > int(Wd) || l < 0.0;
-            sumlo += wlo;
-        };
-        if (lane < M) one(lane, c0, v0, lb);
-        for (int i = lane + 64; i < M; i += 64) one(i, B.col_idx[eqs + i], B.val[eqs + i], B.col_lb[h.co + i]);
-        bad = wave_or(bad | (infeas << 1));
-        sumlo = wave_sum(sumlo);
-        const int W = int(Wd);
-        if (bad & 1) status = HALDA_STATUS_UNSUPPORTED;
-        else if ((bad & 2) || sumlo > W || (M == 0 && W > 0)) status = HALDA_STATUS_INFEASIBLE;
-        else if (M == 0) status = 1000;  // no devices and W = 0: optimal, x = [C = 0]
-        else {
-            const int R1 = W - sumlo + 1;
-            const bool kc = cC > 0.0;
-            if (R1 > r1max || int64_t(M) * odd_stride(R1) > (kc ? tab_kc : tab)) status = HALDA_STATUS_TOO_LARGE;
-            else verdict = kc ? CLS_GEN : (M > kK1MaxM ? CLS_GEN1 : CLS_K1);
-        }
-    }
-    if (lane == 0) {
-        cls[inst] = uint8_t(verdict);
-        if (verdict == CLS_DONE) {
-            if (status == 1000) {
-                Rz.x[h.co] = 0.0;
-                Rz.status[inst] = HALDA_STATUS_OPTIMAL;
-                Rz.obj_lin[inst] = Rz.dual_bound[inst] = Rz.gap[inst] = 0.0;
-                Rz.nodes[inst] = 0;
-            } else {
-                write_done(Rz, int(inst), status, 0);
-            }
-        }
-    }
-    return verdict;
-}
-
-// XCD-aware block -> instance map (bijective for any grid): blocks are dealt round-robin
-// over the 8 XCDs (observed placement, speed only), so block b works on instance
-// (b % 8) * ~(n / 8) + b / 8 -- each XCD walks one contiguous range of instances in
-// order, and the instances of one fleet (adjacent, sharing their CSR) meet in one L2.
-__device__ inline int64_t xcd_swizzle(int64_t b, int64_t n) {
-    const int64_t x = b % 8, q = n / 8, r = n % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-// Screen + k = 1 fast path, one wave per instance: a settled instance's wave
-// exits after three round trips, so the hardware dispatcher refills its slot at
-// once and the (fewer, longer) solves stay evenly spread over the chip whatever
-// the order of the survivors in the batch. k > 1 and wide instances, and the
-// fast path's hand-backs, go to halda_solve_kernel (launched next) through cls.
-__global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_screen_k1_kernel(halda_batch B, halda_result Rz,
-                                                                                       uint8_t *cls, int mmax,
-                                                                                       int r1max, int tab, int tab_kc,
-                                                                                       int *hb_flag, int launch_id,
-                                                                                       int swz) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x;
-    const int64_t inst = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : int64_t(blockIdx.x);
-    HALDA_WSTAMP(7, __builtin_amdgcn_s_memtime());
-    HALDA_WSTAMP(8, __builtin_amdgcn_s_memrealtime());
-    Head h;
-    if (screen_one(B, Rz, cls, inst, lane, mmax, r1max, tab, tab_kc, h) != CLS_K1) {
-        HALDA_WSTAMP(9, __builtin_amdgcn_s_memrealtime());
-        return;
-    }
-    const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
-    WaveCtx w = {};
-    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
-    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
-    w.cost = reinterpret_cast<double *>(smem + sl.cost);
-    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
-    Inst I;
-    I.inst = int(inst);
-    I.m = h.m;
-    I.M = h.M;
-    I.iC = 7 * h.M;
-    I.invM = 1.0f / float(h.M);
-    I.co = h.co;
-    I.ro = h.ro;
-    I.rp = B.row_ptr + h.cs;
-    I.Wd = h.Wd;
-    I.W = int(h.Wd);
-    I.kc = h.kc;
-    solve_k1(B, Rz, cls, w, smem + sl.stage, smem + sl.stage + kStageColBytes, I, lane, hb_flag, launch_id);
-    HALDA_WSTAMP(9, __builtin_amdgcn_s_memrealtime());
-}

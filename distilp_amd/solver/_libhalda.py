@@ -321,8 +321,6 @@ class HaldaContext:
         rc = self.lib.halda_last_phase_ms(self.ctx, ms)
         if rc != 0:
             raise RuntimeError(f"halda_last_phase_ms failed ({rc}): {last_error(self.lib)}")
-        if os.environ.get("HALDA_TWO_PASS", "") == "0":  # the fused layout
-            return {"halda_screen_k1_kernel": ms[0], "halda_solve_kernel": ms[2]}
         return {"halda_screen_kernel": ms[0], "halda_solve_k1_kernel": ms[1], "halda_solve_kernel": ms[2]}
 
 

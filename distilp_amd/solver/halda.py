@@ -25,6 +25,7 @@ forms every objective on the host the same way (vectorised offsets, one NumPy do
 
 from __future__ import annotations
 
+import numbers
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -36,8 +37,15 @@ from .fleets import _PACKER, fleet_constants, fleet_table, pack_one, solve_table
 from .lower import kv_bits_to_factor
 
 
+def _as_k(k):
+    """A k-candidate as ILPResult(k=...) would store it (pydantic's int coercion,
+    dense_common.py:233-237): integers of any integral type (numpy's too) become int; anything
+    else is left for the reference's own arithmetic (W = L // k) to reject."""
+    return int(k) if isinstance(k, numbers.Integral) else k
+
+
 def _k_list(model: ModelProfile, k_candidates: Optional[Iterable[int]]) -> List[int]:
-    return sorted(set(k_candidates)) if k_candidates else valid_factors_of_L(model.L)
+    return sorted({_as_k(k) for k in k_candidates}) if k_candidates else valid_factors_of_L(model.L)
 
 
 def _offset_parts(devs, model: ModelProfile, sets) -> Tuple[float, float, float]:
@@ -262,7 +270,7 @@ def halda_solve_batch(
     Returns one HALDAResult per fleet, or None where no k is feasible (where
     `halda_solve` would raise). Prints nothing."""
     if k_candidates:
-        Ks = sorted(set(k_candidates))
+        Ks = sorted({_as_k(k) for k in k_candidates})
     else:
         L = model.L
         Ks = sorted({d for d in range(1, L) if L % d == 0}) if L > 1 else []

@@ -10,6 +10,9 @@ R=${1:-r02}
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_$R
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# the library these passes profile (pmc_summary.py keys the summary to it; bench.py uses a summary
+# only for the libhalda.so it loads)
+sha256sum distilp_amd/libhalda.so | cut -d' ' -f1 > "$OUT/lib_sha256"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --streams 1 > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- \

@@ -201,3 +201,42 @@ def test_torch_still_sees_the_gpu_after_libhalda():
             "x = torch.ones(8, device='cuda'); print(float(x.sum()))")
     r = subprocess.run([sys.executable, "-c", code], cwd=str(REPO), capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and r.stdout.strip().endswith("8.0"), r.stderr[-2000:]
+
+
+def test_c_abi_objective_against_halda_solve(fixtures_golden, llama_online_model):
+    """What a C / C++ caller of halda_solve_fleets gets ("objective"): obj_value formed on
+    the GPU (c.x in a fixed tree order), the best k picked with it. Against halda_solve (the reference's
+    formula, halda_p_solver.py:356-357, c.x by NumPy on the host): obj_value within 1e-12 relative and the
+    same best k wherever the best two k's objectives are more than 1e-12 apart (the documented near-tie
+    caveat), on the 24 fixture cases and 1,024 C3 fleets."""
+    import contextlib
+    import io
+
+    from distilp_amd.solver import halda_solve
+    from distilp_amd.solver.lower import kv_bits_to_factor
+
+    cases = []
+    for fx in fixtures_golden["fixtures"].values():
+        devs, model = fixture_fleet(fx["folder"])
+        cases.append(([devs], model, fx["kv_bits"]))
+    cases.append(([[DeviceProfile.model_validate(d) for d in synth_fleet(s, 64)] for s in range(1024)],
+                  llama_online_model, "4bit"))
+    n_cmp = n_bits = 0
+    for fleets, model, kv in cases:
+        with contextlib.redirect_stdout(io.StringIO()):
+            from distilp_amd.solver.coefficients import valid_factors_of_L
+            ks = sorted(valid_factors_of_L(model.L))
+        res = solve_table(fleet_table(fleets, model), model, ks, kv_bits_to_factor(kv))
+        for f, devs in enumerate(fleets):
+            with contextlib.redirect_stdout(io.StringIO()):
+                want = halda_solve(devs, model, mip_gap=1e-4, plot=False, kv_bits=kv)
+            got = float(res.obj_value[f])
+            assert abs(got - want.obj_value) <= 1e-12 * max(1.0, abs(want.obj_value)), (f, got, want.obj_value)
+            obk = np.sort(res.obj_by_k[f][np.isfinite(res.obj_by_k[f])])
+            near = len(obk) > 1 and obk[1] - obk[0] <= 1e-12 * max(1.0, abs(obk[0]))
+            if not near:
+                assert int(res.best_k[f]) == want.k, (f, int(res.best_k[f]), want.k)
+            n_cmp += 1
+            n_bits += got == want.obj_value
+    assert n_cmp == 24 + 1024
+    print(f"C ABI obj_value bit-equal to halda_solve's on {n_bits} of {n_cmp}")

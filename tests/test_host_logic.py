@@ -386,3 +386,14 @@ def test_bench_gpus_n_spawns_one_rank_per_gpu(monkeypatch):
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
     assert "--backend" not in cmd  # nccl (RCCL) is the default backend of the ranks
+
+
+def test_k_candidates_are_stored_as_int(llama_online_model):
+    """k-candidates of any integral type (numpy's too) are deduplicated, sorted and kept as int, as
+    ILPResult(k=...) coerces them in the reference (dense_common.py:233-237)."""
+    import numpy as np
+
+    from distilp_amd.solver.halda import _k_list
+
+    ks = _k_list(llama_online_model, [np.int64(4), 2, np.int32(2), 1])
+    assert ks == [1, 2, 4] and all(type(k) is int for k in ks)

@@ -62,7 +62,9 @@ def main(R):
         return statistics.median(next(v for k, v in cal.items() if k.startswith(prefix))) * 1024 / calib_bytes
 
     f8, f16 = pick("read8"), pick("read16")
-    out = {"fetch_size_over_bytes_8B_per_lane": f8, "fetch_size_over_bytes_16B_per_lane": f16, "kernels": {}}
+    sha = (src / "lib_sha256").read_text().strip() if (src / "lib_sha256").exists() else None
+    out = {"libhalda_sha256": sha, "fetch_size_over_bytes_8B_per_lane": f8,
+           "fetch_size_over_bytes_16B_per_lane": f16, "kernels": {}}
     for name in fetch:
         if "halda" not in name:
             continue
@@ -73,8 +75,7 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-    solve = (out["kernels"].get("halda_sweep_kernel") or out["kernels"].get("halda_screen_k1_kernel")
-             or out["kernels"].get("halda_solve_k1_kernel"))
+    solve = out["kernels"].get("halda_sweep_kernel") or out["kernels"].get("halda_solve_k1_kernel")
     out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
     out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
                    "coalesced read (tools/hbm_calib.hip), the solve kernel's dominant access width; "
