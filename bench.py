@@ -495,6 +495,52 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     }
 
 
+def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
+    """Latency mode (halda_p_solver.py:391-412 is the k loop it shards): the k-sweep of
+    one C2 fleet and of 4096 C2 fleets through halda_solve_fleets_sharded over a real one-rank RCCL
+    communicator (the three device all-reduces and the shard kernels included) against the plain
+    sweep, and the same step sequence for 2 / 4 / 8 virtual ranks on this one GPU
+    (halda_solve_fleets_sharded_emulated: every rank's sub-sweep runs here one after another and each
+    all-reduce is a device reduction, so it prices the extra launches, not an 8-GPU latency). Per
+    call: device ms from HIP events around `runs` back-to-back calls on one stream, and the wall ms
+    of one synchronous call (enqueue -> results on the device, median)."""
+    from distilp_amd.solver.fleets import (DeviceFleetTable, RcclComm, fleet_table, launch_sharded,
+                                           launch_sharded_emulated)
+
+    out = {"what": latency_leg.__doc__.split("\n\n")[0].replace("\n    ", " ").strip()}
+    try:
+        comm = RcclComm(1, 0, RcclComm.unique_id(), dev.index or 0)
+    except Exception as e:  # noqa: BLE001
+        comm = None
+        out["rccl_error"] = str(e)[:200]
+    sref = stream.cuda_stream
+    for name, n in (("one_fleet", 1), ("fleets_4096", C3_FLEETS)):
+        table = fleet_table(build_fleets(range(50_000, 50_000 + n), 16), model)
+        dt = DeviceFleetTable(table, model, KS_L80, 0.5, dev)
+        ways = {"plain": lambda: dt.launch(ctx, sref)}
+        if comm is not None:
+            ways["rccl_world1"] = lambda: launch_sharded(dt, ctx, comm, sref)
+        for w in (2, 4, 8):
+            ways[f"emulated_world{w}"] = (lambda w=w: launch_sharded_emulated(dt, ctx, w, 0, sref))
+        rec = {}
+        for way, fn in ways.items():
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize(dev)
+            ev = timed_events(fn, runs, torch, dev, stream)
+            walls = []
+            for _ in range(min(runs, 30)):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize(dev)
+                walls.append((time.perf_counter() - t0) * 1e3)
+            rec[way] = {"device_ms_per_call": ev, "wall_ms_sync_call": statistics.median(walls)}
+        out[name] = rec
+    if comm is not None:
+        comm.close()
+    return out
+
+
 def launch_ranks(args) -> int:
     """--gpus N from a plain `python bench.py`: start N ranks (one process per GPU) with
     torch.distributed.run before this process touches the GPU, relay their output and exit code."""
@@ -688,9 +734,10 @@ def main():
     total = inst_rank * world * args.steps if not strong_head else C3_FLEETS * len(ks) * args.steps
     value = total / el_sweep
     n_fleets_total = (len(fleets) * world if not strong_head else C3_FLEETS) * args.steps
-    c2 = None
+    c2 = lat = None
     if world == 1 and not args.no_c2:
         c2 = c2_leg(args, torch, dev, ctx, model, stream, srefs)
+        lat = latency_leg(torch, dev, ctx, model, stream)
     if rank == 0:
         tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
@@ -744,6 +791,7 @@ def main():
                 "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
             },
             "c2": c2,
+            "latency_mode": lat,
             "c5_stream": c5,
             "batch_api": bapi,
             "cpu_baseline": cpu_base,

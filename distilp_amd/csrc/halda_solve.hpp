@@ -75,45 +75,59 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     if (N < 1 || (N - 1) % 7 != 0 || m < 1) status = HALDA_STATUS_UNSUPPORTED;
     const int M = status ? 0 : (N - 1) / 7;
     if (!status && M > mmax) status = HALDA_STATUS_TOO_LARGE;
-    // round trip 2: equality-row extent and bounds, c[C] (lane g), and the w bounds of
-    // every instance of the group (lane = device)
+    // round trip 2: equality-row extent and bounds, c[C] (lane g)
     const int ma = max(m0, 1);
     const int32_t *rp = B.row_ptr + cs0;
     const int eqs0 = rp[ma - 1], eqe0 = rp[ma];
     const double Wd0 = B.row_ub[ro0 + ma - 1], Wl0 = B.row_lb[ro0 + ma - 1];
     const double cC0 = B.c[co0 + 7 * int64_t(max(M, 0))];
-    double lbv[kScreenPer];
-    int Mg_[kScreenPer];
-#pragma unroll
-    for (int g = 0; g < kScreenPer; ++g) {
-        const int Mg = __shfl(M, g);
-        const int64_t cg = shfl64(co0, g);
-        const int64_t idx = cg + (lane < Mg ? lane : 0);
-        lbv[g] = B.col_lb[idx];  // w upper bounds are left to the solve
-        Mg_[g] = Mg;
-    }
     const bool live = own && !status;
     const int eqs = live ? eqs0 : 0, eqe = live ? eqe0 : 0;
     const double Wd = live ? Wd0 : 0.0, Wl = live ? Wl0 : 0.0, cC = live ? cC0 : 0.0;
     if (!status && (!(Wl == Wd) || !(Wd >= 0.0 && Wd < 1e6 && Wd == floor(Wd)) || eqe - eqs != M))
         status = HALDA_STATUS_UNSUPPORTED;
 
-    // round trip 3: equality row entries per instance g (lane = device); lanes
-    // without an entry read the first entry of an open instance's row (valid)
+    // round trip 3, per instance g (lane = device): its equality row entries -- loaded once for a run of
+    // instances sharing the row (the k-instances of one fleet share its CSR) -- and the first
+    // pre = min(M, W + 1) w lower bounds. Each bound is >= 0 or makes the instance infeasible by itself
+    // (lb < 0, and ceil(lb) > W, are infeasible; NaN counts 0), so when those first bounds already need
+    // more than W layers the instance is infeasible whatever the others are (bound infeasibility, M > W
+    // = L / k: 8 of the 9 C3 instances), and the others are read only when they do not.
     int cv[kScreenPer];
     double vv[kScreenPer];
+    double lbv[kScreenPer];
+    int pre_[kScreenPer];
     const uint64_t open = __ballot(lane < kScreenPer && own && !status && M > 0);
     const int safe = open ? __shfl(eqs0, __builtin_ctzll(open)) : 0;
+    const int64_t safe_c = open ? shfl64(co0, __builtin_ctzll(open)) : 0;
+    int e_prev = -1, m_prev = -1;
 #pragma unroll
     for (int g = 0; g < kScreenPer; ++g) {
         const int stg = __shfl(status, g), eg = __shfl(eqs0, g);
-        const bool in = open && i0 + g < B.n_inst && stg == 0 && lane < Mg_[g];
-        const int idx = in ? eg + lane : safe;
-        const int c0 = open ? B.col_idx[idx] : 0;
-        const double v0 = open ? B.val[idx] : 1.0;
-        cv[g] = in ? c0 : lane;
-        vv[g] = in ? v0 : 1.0;
-        if (!in) lbv[g] = 0.0;
+        const int Mg = __shfl(M, g);
+        const int64_t cg = shfl64(co0, g);
+        const int Wg = int(__shfl(Wd, g));
+        const bool og = open && i0 + g < B.n_inst && stg == 0;  // wave-uniform
+        const bool in = og && lane < Mg;
+        const int pre = og ? min(Mg, Wg + 1) : 0;
+        pre_[g] = pre;
+        if (g > 0 && og && eg == e_prev && Mg == m_prev) {  // the same row as the previous open instance
+            cv[g] = cv[g - 1];
+            vv[g] = vv[g - 1];
+        } else {
+            const int idx = in ? eg + lane : safe;
+            const int c0 = open ? B.col_idx[idx] : 0;
+            const double v0 = open ? B.val[idx] : 1.0;
+            cv[g] = in ? c0 : lane;
+            vv[g] = in ? v0 : 1.0;
+        }
+        if (og) {
+            e_prev = eg;
+            m_prev = Mg;
+        }
+        const bool lin = og && lane < pre;
+        const double l0 = open ? B.col_lb[lin ? cg + lane : safe_c] : 0.0;
+        lbv[g] = lin ? l0 : 0.0;
     }
     int verdict = CLS_DONE, vstatus = status;  // lane g: outcome of instance g
 #pragma unroll
@@ -121,20 +135,33 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
         if (i0 + g >= B.n_inst) break;
         const int stg = __shfl(status, g);
         if (stg) continue;
-        const int Mg = __shfl(M, g), eg = __shfl(eqs, g);
+        const int Mg = __shfl(M, g), eg = __shfl(eqs, g), pre = pre_[g];
         const int64_t cg = shfl64(co, g);
         const double Wg = __shfl(Wd, g);
         int bad = 0, infeas = 0, sumlo = 0;
-        auto one = [&](int i, int col, double v, double lb) {
-            bad |= col != i || v != 1.0;
+        auto lbone = [&](double lb) {
             const int wlo = int(ceil(lb));
             infeas |= wlo > int(Wg) || lb < 0.0;
             sumlo += wlo;
         };
-        if (lane < Mg) one(lane, cv[g], vv[g], lbv[g]);
-        for (int i = lane + 64; i < Mg; i += 64) one(i, B.col_idx[eg + i], B.val[eg + i], B.col_lb[cg + i]);
+        if (lane < Mg) bad |= cv[g] != lane || vv[g] != 1.0;
+        for (int i = lane + 64; i < Mg; i += 64) bad |= B.col_idx[eg + i] != i || B.val[eg + i] != 1.0;
+        if (lane < pre) lbone(lbv[g]);
+        for (int i = lane + 64; i < pre; i += 64) lbone(B.col_lb[cg + i]);
         bad = wave_or(bad | (infeas << 1));
         sumlo = wave_sum(sumlo);
+        if (!bad && sumlo <= int(Wg) && pre < Mg) {  // the first bounds prove nothing: the rest of them
+            infeas = 0;
+            int rest = 0;
+            for (int i = pre + lane; i < Mg; i += 64) {
+                const double lb = B.col_lb[cg + i];
+                const int wlo = int(ceil(lb));
+                infeas |= wlo > int(Wg) || lb < 0.0;
+                rest += wlo;
+            }
+            bad = wave_or(infeas << 1);
+            sumlo += wave_sum(rest);
+        }
         const int W = int(Wg);
         int st = 0, v = CLS_DONE;
         if (bad & 1) st = HALDA_STATUS_UNSUPPORTED;
@@ -1076,6 +1103,13 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     // decreases, so a device that is not useful now never becomes useful except the one that just
     // took a unit; the scan therefore jumps T straight to the next useful opening and costs one
     // reduction per exchange instead of one per candidate T.
+    // That holds in exact arithmetic. In floating point a leaf that is linear over a stretch (equal
+    // increments: the same device twice, a homogeneous cluster) has increments that differ by
+    // rounding, so "gn < lam" may become true for a device only after lam was re-formed from its own
+    // twin's equal unit -- an opening whose H lies below the T already reached. T therefore never
+    // decreases: such an opening is taken at the current T (its H is <= T, so it is allowed there), and
+    // the recorded kc T + S stays the cost of an allocation whose cycle times are all <= T. The
+    // exchanges it allows change S by rounding only.
     double hn = act && cap < hi ? H[cap + 1] : kInf;   // H of this device's next cap
     double gn = act && cap < hi ? G[cap + 1] - G[cap] : kInf;  // the unit it opens (cap -> cap + 1)
     double lt = act && e > lo ? G[e] - G[e - 1] : -kInf;  // its last taken unit
@@ -1094,7 +1128,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
         const bool useful = act && e == cap && cap < hi && (need > 0 || gn < lam);
         const double cand = useful ? hn : kInf;
         const double Tn = sg.min_f64(cand);
-        if (!(Tn < kInf) || !(kc * Tn + s_inf < best) || Tn > t_stop) break;
+        const double Te = fmax(T, Tn);  // (+inf when no opening is left)
+        if (!(Tn < kInf) || !(kc * Te + s_inf < best) || Te > t_stop) break;
         const int li = sg.lowest(cand == Tn);
         ++events;
         const double d = sg.bcast(gn, li);
@@ -1122,7 +1157,7 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             lam = sg.max_f64(lt);
             lj = sg.highest(lt == lam);
         }
-        T = Tn;
+        T = Te;
         if (need == 0 && kc * T + S < best) {
             best = kc * T + S;
             bestE = e;

@@ -135,7 +135,7 @@ static int dp2(problem *p, int use_T, double T, top2 *opts, cell *dp, int *sol_w
         cell *prev = &dp[(size_t)i * stride], *cur = &dp[(size_t)(i + 1) * stride];
         for (int v = 0; v <= W; v++) {
             cur[v].cnt = 0;
-            for (int w = 1; w <= v; w++) {
+            for (int w = 0; w <= v; w++) {  /* opts hold only w in [lb, ub] */
                 top2 *t = &opts[i * stride + w];
                 cell *pc = &prev[v - w];
                 for (int o = 0; o < t->cnt; o++)
@@ -263,7 +263,11 @@ int halda_exact_solve(int n, int m, const double *A, const double *bl, const dou
         if (dr[i].have1 != 1 || dr[i].have2 != 1) status = EX_UNSUPPORTED;
     for (int j = 2 * M; j < 6 * M && status == EX_OK; j++)
         if (c[j] < 0) status = EX_UNSUPPORTED;
-    if (status == EX_OK && M > W) status = EX_INFEASIBLE; /* w_i >= 1 */
+    if (status == EX_OK) { /* bound infeasibility: sum_i ceil(lb(w_i)) > W (M > W for the reference's lb = 1) */
+        long long sumlo = 0;
+        for (int i = 0; i < M; i++) sumlo += wlo[i];
+        if (sumlo > W) status = EX_INFEASIBLE;
+    }
     if (status == EX_OK && M == 0) status = W == 0 ? EX_OK : EX_INFEASIBLE;
     if (status != EX_OK || M == 0) {
         free(dr); free(wlo);

@@ -367,3 +367,46 @@ def test_csr_batches_on_several_streams(llama_online_model, n_streams):
         assert np.array_equal(out["status"].cpu().numpy(), want.status)
         assert np.array_equal(out["x"].cpu().numpy(), want.x)
         assert np.array_equal(out["obj_lin"].cpu().numpy(), want.obj_lin)
+
+
+@pytest.mark.parametrize("case", ["lowered", "zero_prefix", "neg_tail", "nan_tail"])
+def test_screen_bound_infeasibility_from_a_prefix(llama_online_model, case):
+    """The screen proves bound infeasibility (sum_i ceil(lb(w_i)) > W, HiGHS's presolve verdict) from the
+    first min(M, W + 1) w lower bounds when they already exceed W (every bound is >= 0 or infeasible by
+    itself), reading the others only when they do not. M = 16 at k = 8 (W = 10 < M): as lowered it is
+    infeasible from the prefix; with the first 11 bounds 0 the rest decide (sum 5 <= 10: solved, against
+    the exact oracle); a negative or NaN bound past the prefix does not change the verdict. k = 1 (W = 80:
+    the prefix is every bound) is solved as usual."""
+    from distilp_amd.common import DeviceProfile
+
+    M = 16
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(77, M)]
+    fl = lower_fleet(devs, llama_online_model, "4bit")
+    ks = [1, 8]
+    batch, refs = assemble([fl], [ks])
+    batch.col_lb = batch.col_lb.copy()
+    probs = []
+    for ref in refs:
+        p = mo.lower_dense(devs, llama_online_model, ref.k, 0.5)
+        p["lb"] = p["lb"].copy()
+        if ref.k == 8:
+            if case == "zero_prefix":
+                for i in range(11):
+                    batch.col_lb[ref.col_off + i] = p["lb"][i] = 0.0
+            elif case == "neg_tail":
+                batch.col_lb[ref.col_off + 15] = p["lb"][15] = -1.0
+            elif case == "nan_tail":
+                batch.col_lb[ref.col_off + 15] = np.nan
+        probs.append(p)
+    batch.max_cols = batch.max_R1 = batch.max_tab = batch.max_tab_kc = 0  # summary from the bounds (host API)
+    res = get_context(0).solve(batch)
+    for j, (ref, p) in enumerate(zip(refs, probs)):
+        if ref.k == 8 and case != "zero_prefix":
+            assert res.status[j] == STATUS_INFEASIBLE, (case, res.status[j])
+            continue
+        st, xo, b1, b2, _ = mo.exact_solve(p)
+        assert st == 0 and res.status[j] == STATUS_OPTIMAL, (case, ref.k, st, res.status[j])
+        assert _obj_close(float(res.obj_lin[j]), b1), (case, ref.k)
+        x = res.x[ref.col_off:ref.col_off + ref.n_cols]
+        if mo.uniqueness_margin_ok(b1, b2):
+            assert np.array_equal(x[:2 * M], xo[:2 * M])

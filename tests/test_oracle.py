@@ -108,3 +108,23 @@ def test_exact_oracle_matches_highs_on_tied_fleets(llama_online_model):
             assert a["k"] == b["k"] and a["success"] == b["success"]
             if a["success"]:
                 assert abs(a["obj_value"] - b["obj_value"]) <= 1e-9 * max(1.0, abs(b["obj_value"]))
+
+
+def test_exact_oracle_matches_highs_with_zero_w_bounds(llama_online_model):
+    """Outside the reference's own instances (it always sets lb(w) = 1): w lower bounds of 0 on some
+    devices (the screen's bound-prefix test, test_gpu_parity.py). The exact solver's DP and its
+    bound-infeasibility check follow the bounds, not w >= 1: the same status and objective as HiGHS."""
+    from .helpers import synth_devices  # noqa: F401
+    from distilp_amd.common import DeviceProfile
+    from distilp_amd.synth import synth_fleet
+
+    devs = [DeviceProfile.model_validate(d) for d in synth_fleet(77, 16)]
+    for k, nz in ((8, 11), (8, 4), (1, 11), (5, 16), (16, 16)):
+        p = mo.lower_dense(devs, llama_online_model, k, 0.5)
+        p["lb"] = p["lb"].copy()
+        p["lb"][:nz] = 0.0
+        st, _, b1, _, _ = mo.exact_solve(p)
+        r = mo.highs_solve(p)
+        assert (st == 0) == (r.status == 0), (k, nz, st, r.status)
+        if st == 0:
+            assert abs(b1 - r.fun) <= 1e-9 * max(1.0, abs(r.fun)), (k, nz, b1, r.fun)

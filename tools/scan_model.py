@@ -77,7 +77,8 @@ def scan_range(G, H, kc, t_start=None, t_stop=INF):
         if not c:
             break
         Tn, li = min(c)
-        if not (kc * Tn + s_inf < best) or Tn > t_stop:
+        Te = max(T, Tn)  # T never decreases (see kc_scan_incremental)
+        if not (kc * Te + s_inf < best) or Te > t_stop:
             break
         events += 1
         d = G[li][cap[li] + 1] - G[li][cap[li]]
@@ -91,7 +92,7 @@ def scan_range(G, H, kc, t_start=None, t_stop=INF):
         e[li] += 1
         if nd == 0:
             lam, lj = lam_of()
-        T = Tn
+        T = Te
         if nd == 0 and kc * T + S < best:
             best, bestT = kc * T + S, T
     return best, bestT, events
@@ -221,7 +222,8 @@ def model(G, H, kc, W):
         if not cands:
             break
         Tn, li = min(cands)
-        if not (kc * Tn + s_inf < best):
+        Te = max(T, Tn)
+        if not (kc * Te + s_inf < best):
             break
         events += 1
         d = G[li][cap[li] + 1] - G[li][cap[li]]
@@ -235,7 +237,7 @@ def model(G, H, kc, W):
         e[li] += 1
         if nd == 0:
             lam, lj = lam_of()
-        T = Tn
+        T = Te
         if nd == 0 and kc * T + S < best:
             best = kc * T + S
     return {"best": best, "brute": bestF, "events": events, "nT": nT, "n_cand": len(Ts), "need": need,
