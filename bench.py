@@ -573,6 +573,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tto", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 leg (4096 M = 16 fleets)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the latency-mode leg")
     ap.add_argument("--ks", type=str, default="", help="diagnostic: comma-separated k-candidates instead of C3's")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-core", type=int, default=0)
@@ -737,7 +738,7 @@ def main():
     c2 = lat = None
     if world == 1 and not args.no_c2:
         c2 = c2_leg(args, torch, dev, ctx, model, stream, srefs)
-        lat = latency_leg(torch, dev, ctx, model, stream)
+        lat = None if args.no_latency else latency_leg(torch, dev, ctx, model, stream)
     if rank == 0:
         tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
