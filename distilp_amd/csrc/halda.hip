@@ -75,9 +75,9 @@ struct Ctx {
     bool fleet_seg = false;                      // fused sweep: the first launch was the segment kernel
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
-    int kslot_split = 2;                         // k-slot launch: the longest scan split over this many waves
-    int kslot_split_env = 2;                     // its value from HALDA_KSLOT_SPLIT (fleets path 1 restores it)
-    int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters)
+    int kslot_split = 2;                         // k-slot launch: the longest scan split over 2 waves (0: unsplit)
+    int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters; 2.5x
+                                                 // measured best of 4..12)
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
@@ -845,11 +845,6 @@ int halda_init(int device_ordinal, void **ctx_out) {
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
-    const char *ks = std::getenv("HALDA_KSLOT_SPLIT");  // parts of the k-slot scan split: 0 / 1 off, 2, 3
-    c->kslot_split = ks ? std::max(0, std::min(std::atoi(ks), kMaxSplitParts)) : 2;
-    c->kslot_split_env = c->kslot_split;
-    const char *cw = std::getenv("HALDA_KSLOT_CRIT_W");
-    c->kslot_crit_w4 = cw ? std::max(1, std::min(std::atoi(cw), 16)) : 10;  // 2.5x (measured best of 4..12)
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
@@ -951,15 +946,15 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
 int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    if (path < 0 || path > 6)
+    if (path < 0 || path > 5)
         return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave), 3 (fused, k = 1 "
-                                 "by DP), 4 (fused, segment kernel instead of the k-slot kernel), 5 / 6 (fused, "
-                                 "the k-slot scan unsplit / in three parts)");
+                                 "by DP), 4 (fused, segment kernel instead of the k-slot kernel), 5 (fused, the "
+                                 "k-slot scan unsplit)");
     c->fleets_fused = path != 0;
-    c->seg_sweep = path == 1 || path == 4 || path == 5 || path == 6;
-    c->kslot_sweep = path == 1 || path == 5 || path == 6;
+    c->seg_sweep = path == 1 || path == 4 || path == 5;
+    c->kslot_sweep = path == 1 || path == 5;
     c->k1_force_dp = path == 3;
-    c->kslot_split = path == 5 ? 0 : path == 6 ? 3 : c->kslot_split_env;
+    c->kslot_split = path == 5 ? 0 : 2;
     return HALDA_OK;
 }
 

@@ -983,18 +983,19 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 // false (caller runs the general scan) when a leaf is not convex / monotone.
 // On success st0 holds the allocation (table indices e_i).
 //
-// Split over two or three waves of a k-slot workgroup (16-lane segments only, sp.part != 0): the
-// scan's length is the workgroup's critical path, and each event is a dependent chain of reductions,
-// so the candidate range is cut at T_a (and T_b) and the parts run at once. Part 1 (the slot's own
-// wave) takes the openings T <= T_a; part p > 1 (a helper wave) starts from the optimal capped
-// allocation at its lower cut -- the state the one scan reaches there (the capped optimum is unique
-// when no two devices tie on an increment) -- and takes the openings up to its upper cut, pruning with
-// its own bound (never fewer events than the one scan makes in its range). Part 1 then takes the
-// helpers' allocations in ascending T, each only when strictly better, so the earliest T wins ties as
-// in the one scan. Cuts (tools/scan_model.py on dumped C2 tables, the longest scan per wave): two
-// parts, the lower median over the devices of H at cap(T0) + 2 (47 -> 28 events); three parts, the
-// lower quartile of H at cap(T0) + 2 and the lower median of H at cap(T0) + 3 (-> 21 events).
-constexpr int kMaxSplitParts = 3;
+// Split over two waves of a k-slot workgroup (16-lane segments only, sp.part != 0): the scan's length
+// is the workgroup's critical path, and each event is a dependent chain of reductions, so the
+// candidate range is cut at T_a (the lower median over the devices of H at cap(T0) + 2;
+// tools/scan_model.py on dumped C2 tables: the longest scan per wave 47 -> 28 events) and the two
+// parts run at once. Part 1 (the slot's own wave) takes the openings T <= T_a; part 2 (a helper wave)
+// starts from an optimal capped allocation at T_a (the greedy's) and takes the openings above it,
+// pruning with its own bound. Under ties (repeated devices) that allocation need not be the one the
+// one scan holds at T_a, and it does not have to be: an exchange keeps ANY optimal capped allocation
+// optimal (its largest taken increment lam and the set of useful openings are the same for every
+// optimal allocation), and T never decreases (above), so part 2 prices the same S(T) as the one scan
+// from T_a on (tests/test_scan_split_model.py, tests/test_gpu_ties.py). Part 1 then takes part 2's
+// allocation only when strictly better, so the earliest T wins ties as in the one scan.
+constexpr int kMaxSplitParts = 2;
 struct SplitArea {  // per segment, in LDS
     // part 1 -> the helpers, after its leaf scan and phase-0 greedy (the helpers repeat neither)
     double s_inf, best0;
@@ -1007,8 +1008,8 @@ struct SplitArea {  // per segment, in LDS
     int alt_e[kMaxSplitParts - 1][16];    // part p's allocation (one int per segment lane)
 };
 struct ScanSplit {
-    int part = 0;     // 0: no split, 1: the slot's own wave, 2 / 3: a helper
-    int n_parts = 0;  // 2 or 3
+    int part = 0;     // 0: no split, 1: the slot's own wave, 2: the helper
+    int n_parts = 0;  // 2 (split) or 0
     SplitArea *ar = nullptr;
 };
 
@@ -1050,20 +1051,11 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             const double v2 = has ? H[min(cap + 2, hi)] : kInf;
             const int n = sg.sum_i(has ? 1 : 0);
             const int r2 = rank16(v2, lane, std::make_integer_sequence<int, 15>{});
-            double ta, tb = kInf;  // cuts > T0; +inf: no opening at all
-            if (sp.n_parts == 2) {
-                ta = sg.min_f64(has && r2 == (n - 1) / 2 ? v2 : kInf);
-            } else {
-                const double v3 = has ? H[min(cap + 3, hi)] : kInf;
-                const int r3 = rank16(v3, lane, std::make_integer_sequence<int, 15>{});
-                const double a = sg.min_f64(has && r2 == (n - 1) / 4 ? v2 : kInf);
-                const double b = sg.min_f64(has && r3 == (n - 1) / 2 ? v3 : kInf);
-                ta = fmin(a, b);
-                tb = fmax(a, b);
-            }
-            t_stop = part == 1 ? ta : part == 2 ? tb : kInf;
+            // the cut (> T0; +inf: no opening at all)
+            const double ta = sg.min_f64(has && r2 == (n - 1) / 2 ? v2 : kInf);
+            t_stop = part == 1 ? ta : kInf;
             if (part > 1) {
-                T = part == 2 ? ta : tb;
+                T = ta;
                 if (act)
                     while (cap < hi && H[cap + 1] <= T) ++cap;
             }

@@ -1312,8 +1312,8 @@ struct SlotArgs {
     int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
     int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
     int helper;                // slot whose threshold scan is split over n_parts waves (-1: none)
-    int n_parts;               // 2 or 3
-    int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 / 3 first: a light slot's, or n_slot
+    int n_parts;               // 2 (split) or 0
+    int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
 };

@@ -286,7 +286,7 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
-    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3, "seg": 4, "kslot_unsplit": 5, "kslot_split3": 6}
+    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3, "seg": 4, "kslot_unsplit": 5}
 
     def set_fleets_path(self, path) -> None:
         """halda_solve_fleets on the fused sweep ("fused" / True, default: fleets of at most 16 devices
@@ -294,7 +294,7 @@ class HaldaContext:
         (four fleets per wave, every k in turn: "seg"), the fused sweep one fleet per wave ("wave"), the CSR
         pipeline ("csr" / False), or (test paths) the fused sweep with every k = 1 solve of its
         register launch done by the exact DP it falls back to ("dp"), or with the k-slot kernel's
-        k = 2 threshold scan unsplit ("kslot_unsplit") / over three waves ("kslot_split3")."""
+        k = 2 threshold scan unsplit ("kslot_unsplit"; the default splits it over two waves)."""
         code = self.FLEET_PATHS[path] if isinstance(path, str) else int(bool(path))
         rc = self.lib.halda_set_fleets_path(self.ctx, code)
         if rc != 0:

@@ -226,8 +226,8 @@ void halda_fleets_plan_free(void *plan);
  *   (halda_sweep_seg_kernel);
  * 2 the fused sweep, one fleet per wave only;
  * 4 the fused sweep with the segment kernel instead of the k-slot kernel;
- * 5 / 6 (test paths) the fused sweep with the k-slot kernel's k = 2 threshold scan unsplit / split
- *   over three waves (path 1: two, or HALDA_KSLOT_SPLIT);
+ * 5 (test path) the fused sweep with the k-slot kernel's k = 2 threshold scan unsplit (path 1 splits
+ *   it over two waves);
  * 0 the CSR pipeline (lowering kernel -> the halda_solve_batch kernels -> pick kernel), which also
  *   keeps the lowered batch for halda_last_lowered. All give the same statuses, x and k.
  * HALDA_E_ARG for any other path. */

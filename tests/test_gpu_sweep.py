@@ -110,10 +110,9 @@ def test_multi_device_context_equals_single(llama_online_model):
 @pytest.mark.parametrize("path,kernel,sizes", [
     ("fused", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
     ("fused", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
-    # the k = 2 threshold scan unsplit / in three parts (the default splits it in two)
+    # the k = 2 threshold scan unsplit (the default splits it in two)
     ("kslot_unsplit", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
-    ("kslot_split3", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
-    ("kslot_split3", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
+    ("kslot_unsplit", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
     ("seg", "halda_sweep_seg_kernel", [1 + (s * 7) % 16 for s in range(300)]),
 ])
 def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model, path, kernel, sizes):

@@ -8,7 +8,7 @@ exact). These fleets make such ties certain: the reference's own "same device tw
 batches of more than 64 fleets, so halda_solve_fleets takes the default k-slot kernel. Per (fleet, k)
 against the exact oracle (status; c.x and the objective within 1e-9; (w, n) where the optimum is
 unique), the best k against the oracle's sweep (ascending k, strict <, halda_p_solver.py:391-412), and
-the unsplit (path 5) / two-part (default) / three-part (path 6) scans against each other."""
+every other scan layout (unsplit k-slot, segment, one fleet per wave, the CSR pipeline) likewise."""
 
 import contextlib
 import io
@@ -37,6 +37,15 @@ def _ks(model):
         return sorted(valid_factors_of_L(model.L))
 
 
+PATHS = {  # halda_set_fleets_path name -> the launch that must have run
+    "fused": "halda_sweep_kslot_kernel",        # default: k-slot kernel, k = 2 scan split over two waves
+    "kslot_unsplit": "halda_sweep_kslot_kernel",
+    "seg": "halda_sweep_seg_kernel",             # four fleets per wave, every k in turn
+    "wave": "halda_sweep_tables_kernel",         # one fleet per wave (64-lane threshold scan)
+    "csr": "halda_solve_kernel",                 # lowered CSR -> general kernel (k > 1)
+}
+
+
 @pytest.mark.parametrize("folder", FIXTURE_FOLDERS)
 def test_kslot_split_scan_on_tied_fleets(folder):
     twice, model = fixture_twice(folder)
@@ -47,15 +56,14 @@ def test_kslot_split_scan_on_tied_fleets(folder):
     ctx = get_context(0)
     runs = {}
     try:
-        for path in ("fused", "kslot_unsplit", "kslot_split3"):
+        for path, kernel in PATHS.items():
             ctx.set_fleets_path(path)
             ctx.set_timing(True)
             runs[path] = solve_table(table, model, ks, 0.5, want_x=True)
-            assert "halda_sweep_kslot_kernel" in ctx.last_fleet_ms(), path
+            assert kernel in ctx.last_fleet_ms(), (path, ctx.last_fleet_ms())
     finally:
         ctx.set_fleets_path("fused")
         ctx.set_timing(False)
-    res = runs["fused"]
     n_open = n_unique = 0
     for f, devs in enumerate(fleets):
         M = len(devs)
@@ -63,33 +71,28 @@ def test_kslot_split_scan_on_tied_fleets(folder):
         for j, k in enumerate(ks):
             p = mo.lower_dense(devs, model, k, 0.5)
             st, xo, b1, b2, _ = mo.exact_solve(p)
+            for path, res in runs.items():
+                if st == 2:
+                    assert res.status[f, j] == STATUS_INFEASIBLE, (path, f, k)
+                    continue
+                assert res.status[f, j] == STATUS_OPTIMAL, (path, f, k, res.status[f, j])
+                x = res.x[f, j, :p["c"].shape[0]]
+                assert _close(float(np.dot(p["c"], x)), b1), (path, f, k, float(np.dot(p["c"], x)), b1)
+                assert _close(float(res.obj_by_k[f, j]), mo.objective_value(p, x)), (path, f, k)
+                if mo.uniqueness_margin_ok(b1, b2):
+                    assert np.array_equal(x[:2 * M], xo[:2 * M]), (path, f, k)
             if st == 2:
-                assert res.status[f, j] == STATUS_INFEASIBLE, (f, k)
                 continue
-            assert res.status[f, j] == STATUS_OPTIMAL, (f, k, res.status[f, j])
             n_open += 1
-            x = res.x[f, j, :p["c"].shape[0]]
-            assert _close(float(np.dot(p["c"], x)), b1), (f, k, float(np.dot(p["c"], x)), b1)
-            obj = mo.objective_value(p, x)
-            assert _close(float(res.obj_by_k[f, j]), obj), (f, k)
-            if mo.uniqueness_margin_ok(b1, b2):
-                n_unique += 1
-                assert np.array_equal(x[:2 * M], xo[:2 * M]), (f, k)
+            n_unique += mo.uniqueness_margin_ok(b1, b2)
+            obj = mo.objective_value(p, xo)
             if best is None or obj < best[0]:
                 best = (obj, k)
-        assert best is not None and res.best_k[f] == best[1], (f, res.best_k[f], best)
-        a, b = table.dev_off[f], table.dev_off[f + 1]
-        assert int(res.w[a:b].sum()) * int(res.best_k[f]) == model.L  # test_integration.py:112
+        for path, res in runs.items():
+            assert best is not None and res.best_k[f] == best[1], (path, f, res.best_k[f], best)
+            a, b = table.dev_off[f], table.dev_off[f + 1]
+            assert int(res.w[a:b].sum()) * int(res.best_k[f]) == model.L  # test_integration.py:112
     assert n_open >= len(fleets)
-    # the three scan layouts: the same statuses and best k, the same objectives (allocations may differ
-    # only where the optimum is not unique, and then by rounding of the same optimum)
-    for path in ("kslot_unsplit", "kslot_split3"):
-        other = runs[path]
-        assert np.array_equal(other.status, res.status), path
-        assert np.array_equal(other.best_k, res.best_k), path
-        fin = res.status == STATUS_OPTIMAL
-        assert np.allclose(other.obj_by_k[fin], res.obj_by_k[fin], rtol=1e-12, atol=0.0), path
-        assert np.allclose(other.obj_value, res.obj_value, rtol=1e-12, atol=0.0), path
 
 
 @pytest.mark.parametrize("folder", FIXTURE_FOLDERS)
