@@ -84,6 +84,7 @@ struct Ctx {
     bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
     bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
     bool last_fleet_fused = false;
+    int path_gen = 0;              // bumped by halda_set_fleets_path: prepared plans re-plan on their next launch
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
     size_t shard_bytes = 0;
     void *emu = nullptr;           // the other virtual ranks' results of halda_solve_fleets_sharded_emulated
@@ -447,6 +448,9 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
     if (SA.helper >= 0) kslot_lds += int64_t(64 / kSegLanes) * int64_t(sizeof(SplitArea));
+    kslot_lds = align16(kslot_lds);
+    SA.rec_off = int(kslot_lds);
+    kslot_lds += int64_t(sizeof(KslotRecs));
     const bool kslot = c->seg_sweep && c->kslot_sweep && fits && mmax <= kSegLanes && tab_kc > 0 && kslot_all &&
                        SA.n_slot >= 1 && nf > kSweepSmallBatch && kslot_lds <= kLdsBudget;
     const bool seg = !kslot && c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
@@ -955,6 +959,7 @@ int halda_set_fleets_path(void *ctx, int path) {
     c->kslot_sweep = path == 1 || path == 5;
     c->k1_force_dp = path == 3;
     c->kslot_split = path == 5 ? 0 : 2;
+    ++c->path_gen;
     return HALDA_OK;
 }
 
@@ -1032,6 +1037,7 @@ int check_fleets_args(const halda_model *model, const halda_fleets *fleets, cons
 // halda_solve_fleets another way (the CSR pipeline, more than 64 k), the call's arguments.
 struct FleetsPlan {
     Ctx *c = nullptr;
+    int gen = 0;  // the context's path_gen when planned
     bool fused = false;
     SweepPlan p;
     halda_model model;
@@ -1039,6 +1045,15 @@ struct FleetsPlan {
     std::vector<int32_t> ks;
     halda_fleet_result out;
 };
+
+// (Re)derive a plan's launch sequence for its context's current path.
+int replan(FleetsPlan *P) {
+    Ctx *c = P->c;
+    P->gen = c->path_gen;
+    P->fused = P->F.n_fleets > 0 && c->fleets_fused && P->ks.size() <= 64;
+    if (!P->fused) return HALDA_OK;
+    return plan_sweep(c, P->model, P->F, P->ks.data(), int(P->ks.size()), P->out, &P->p);
+}
 }  // namespace
 
 extern "C" {
@@ -1183,13 +1198,10 @@ int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fl
     P->F = *fleets;
     P->ks.assign(ks, ks + std::max(n_k, 0));
     P->out = *out;
-    P->fused = fleets->n_fleets > 0 && c->fleets_fused && n_k <= 64;
-    if (P->fused) {
-        const int rc = plan_sweep(c, *model, *fleets, ks, n_k, *out, &P->p);
-        if (rc != HALDA_OK) {
-            delete P;
-            return rc;
-        }
+    const int rc = replan(P);
+    if (rc != HALDA_OK) {
+        delete P;
+        return rc;
     }
     *plan = P;
     return HALDA_OK;
@@ -1200,10 +1212,14 @@ int halda_fleets_plan_launch(void *plan, void *stream) {
     if (!P) return fail(HALDA_E_ARG, "NULL plan");
     if (P->F.n_fleets <= 0) return HALDA_OK;
     Ctx *c = P->c;
-    if (!P->fused)
-        return halda_solve_fleets(c, &P->model, &P->F, P->ks.data(), int32_t(P->ks.size()), &P->out, stream);
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != c->device) HIP_TRY(hipSetDevice(c->device));
+    if (P->gen != c->path_gen) {  // halda_set_fleets_path since: plan the context's current path
+        const int rc = replan(P);
+        if (rc != HALDA_OK) return rc;
+    }
+    if (!P->fused)
+        return halda_solve_fleets(c, &P->model, &P->F, P->ks.data(), int32_t(P->ks.size()), &P->out, stream);
     return run_sweep(c, P->p, stream ? static_cast<hipStream_t>(stream) : c->stream);
 }
 

@@ -1315,6 +1315,7 @@ struct SlotArgs {
     int n_parts;               // 2 (split) or 0
     int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
+    int rec_off;               // LDS byte offset of the workgroup's device records (KslotRecs)
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
 };
 static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
@@ -1343,6 +1344,46 @@ struct KslotFleet {
     double tsum, xsum, kappa;
     bool anybad;
 };
+
+// The workgroup's device records in LDS: wave 0 forms them (kslot_records) and every other wave of
+// the workgroup reads them, instead of each wave loading the fields and forming the same records again
+// (they are the same four fleets for every slot wave).
+struct KslotRecs {
+    double alpha[64], b[64], p_bp[64], p_b[64], cst[64];
+    int Kset[64], Kvram[64], cg[64];  // cg: cls | gpu << 4
+    double tsum[64 / kSegLanes], kappa[64 / kSegLanes];
+    int anybad[64 / kSegLanes];
+};
+
+__device__ inline void kslot_put_records(KslotRecs *R, const KslotFleet &fd, int lane, int seg) {
+    R->alpha[lane] = fd.me.alpha; R->b[lane] = fd.me.b; R->p_bp[lane] = fd.me.p_bp; R->p_b[lane] = fd.me.p_b;
+    R->cst[lane] = fd.me.cst;
+    R->Kset[lane] = fd.me.Kset; R->Kvram[lane] = fd.me.Kvram; R->cg[lane] = fd.me.cls | (fd.me.gpu << 4);
+    if (lane % kSegLanes == 0) {
+        R->tsum[seg] = fd.tsum;
+        R->kappa[seg] = fd.kappa;
+        R->anybad[seg] = fd.anybad ? 1 : 0;
+    }
+}
+
+__device__ inline KslotFleet kslot_get_records(const SweepArgs &A, const KslotRecs *R, int f, int lane, int seg) {
+    KslotFleet fd;
+    const halda_fleets &F = A.F;
+    fd.d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
+    fd.M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - fd.d0);
+    fd.me.alpha = R->alpha[lane]; fd.me.b = R->b[lane]; fd.me.p_bp = R->p_bp[lane]; fd.me.p_b = R->p_b[lane];
+    fd.me.cst = R->cst[lane];
+    fd.me.Kset = R->Kset[lane]; fd.me.Kvram = R->Kvram[lane];
+    const int cg = R->cg[lane];
+    fd.me.cls = cg & 15;
+    fd.me.gpu = cg >> 4;
+    fd.me.W = 0;
+    fd.tsum = R->tsum[seg];
+    fd.xsum = 0.0;  // fleet_offsets_regs carries every per-device constant in tsum
+    fd.kappa = R->kappa[seg];
+    fd.anybad = R->anybad[seg] != 0;
+    return fd;
+}
 
 __device__ inline KslotFleet kslot_records(const SweepArgs &A, int f, const Seg<kSegLanes> &sg) {
     KslotFleet fd;
@@ -1699,8 +1740,17 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
                          (uint64_t(__builtin_amdgcn_s_getreg((15 << 11) | 4)) << 40) |
                          (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20)) << 56));
     {
+        // the four fleets' device records: formed by wave 0 alone, shared through LDS
+        KslotRecs *recs = reinterpret_cast<KslotRecs *>(smem + SA.rec_off);
         KslotFleet fd = {};
-        if (f < nf) fd = kslot_records(A, int(f), sg);
+        if (q == 0) {
+            if (f < nf) {
+                fd = kslot_records(A, int(f), sg);
+                kslot_put_records(recs, fd, lane, seg);
+            }
+        }
+        __syncthreads();  // the records are in LDS
+        if (q != 0 && f < nf) fd = kslot_get_records(A, recs, int(f), lane, seg);
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
         if (f < nf) kslot_tables(A, SA, q, crit, fd, sg, smem, seg);
         const int my_part = kslot_part_of(SA, q);

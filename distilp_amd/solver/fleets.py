@@ -668,8 +668,8 @@ class DeviceFleetTable:
 
     def plan(self, ctx):
         """The prepared launch of this table on `ctx` (halda_fleets_plan_create: kernel choice, grids and
-        kernel arguments derived once), created on first use and kept with the table; set_fleets_path
-        on ctx afterwards needs replan()."""
+        kernel arguments derived once), created on first use and kept with the table (a set_fleets_path
+        on ctx re-plans it at its next launch)."""
         p = self._plans.get(id(ctx))
         if p is None:
             lib = _bind(ctx.lib)
@@ -685,7 +685,7 @@ class DeviceFleetTable:
         return p
 
     def replan(self) -> None:
-        """Drop the prepared launches (after halda_set_fleets_path on their context)."""
+        """Free the prepared launches (the next launch prepares a new one)."""
         for ctx, h, _ in self._plans.values():
             _bind(ctx.lib).halda_fleets_plan_free(h)
         self._plans.clear()

@@ -209,8 +209,8 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
  * enqueues on `stream` (NULL = the context's stream), asynchronous, with the results of a
  * halda_solve_fleets call on the same arguments. The device arrays behind `fleets` / `out` must stay
  * allocated with the same shapes (n_fleets, dev_off, min / max devices) while the plan lives; their
- * contents may change between launches. The plan keeps the context's path (halda_set_fleets_path) as it
- * was at creation. Launches of one context's plans must be serialised on the host, like every call on
+ * contents may change between launches. A halda_set_fleets_path on the context re-plans the plan at its
+ * next launch. Launches of one context's plans must be serialised on the host, like every call on
  * that context. */
 int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                              int32_t n_k, const halda_fleet_result *out, void **plan);

@@ -347,3 +347,38 @@ def test_prepared_plan_equals_solve_fleets(llama_online_model, sizes):
     assert np.array_equal(dt.out["obj_value"].cpu().numpy(), want2.obj_value)
     assert np.array_equal(dt.out["w"].cpu().numpy(), want2.w)
     dt.replan()
+
+
+def test_prepared_plan_follows_the_context_path(llama_online_model):
+    """A prepared plan re-plans when the context's path changes (halda_set_fleets_path): C2-shaped batch,
+    planned on the k-slot path, then launched on the one-fleet-per-wave and CSR paths -- each runs its
+    own kernels and gives the same statuses, best k and (w, n)."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(24000 + s, 16)] for s in range(100)]
+    table = fleet_table(fleets, llama_online_model)
+    dt = DeviceFleetTable(table, llama_online_model, ks, 0.5, dev, want_per_k=True)
+    stream = torch.cuda.Stream(dev)
+    outs = {}
+    try:
+        ctx.set_timing(True)
+        for path, kernel in (("fused", "halda_sweep_kslot_kernel"), ("wave", "halda_sweep_tables_kernel"),
+                             ("csr", "halda_solve_kernel"), ("fused", "halda_sweep_kslot_kernel")):
+            ctx.set_fleets_path(path)
+            dt.launch(ctx, stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            ms = ctx.last_fleet_ms()
+            assert kernel in ms and (path == "fused") == ("halda_sweep_kslot_kernel" in ms), (path, ms)
+            outs[path] = {k: v.cpu().numpy().copy() for k, v in dt.out.items()}
+    finally:
+        ctx.set_fleets_path("fused")
+        ctx.set_timing(False)
+    for path in ("wave", "csr"):
+        for f in ("status", "best_k", "w", "n"):
+            assert np.array_equal(outs[path][f], outs["fused"][f]), (path, f)
+        assert np.allclose(outs[path]["obj_value"], outs["fused"]["obj_value"], rtol=1e-12, atol=0.0)
