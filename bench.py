@@ -535,6 +535,18 @@ def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
                 torch.cuda.synchronize(dev)
                 walls.append((time.perf_counter() - t0) * 1e3)
             rec[way] = {"device_ms_per_call": ev, "wall_ms_sync_call": statistics.median(walls)}
+        # the critical path a rank of a real world-w node would have: the plain sweep of its own k's alone
+        for w in (2, 4, 8):
+            per_rank = []
+            for r in range(w):
+                sub = KS_L80[r::w]
+                if not sub:
+                    continue
+                ds = DeviceFleetTable(table, model, sub, 0.5, dev)
+                for _ in range(3):
+                    ds.launch(ctx, sref)
+                per_rank.append(timed_events(lambda: ds.launch(ctx, sref), runs, torch, dev, stream))
+            rec[f"rank_subsweep_world{w}"] = {"max_device_ms": max(per_rank), "per_rank_device_ms": per_rank}
         out[name] = rec
     if comm is not None:
         comm.close()
