@@ -468,7 +468,8 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
     p.slice = slice;
     p.scratch = !(reg_mode && !gate);
     SweepArgs &A = p.A;
-    A.Mo = model;
+    static_cast<halda_model &>(A.Mo) = model;
+    A.Mo.bvo = model_bvo(model);
     A.F = F;
     for (int j = 0; j < n_k; ++j) {
         A.ks[j] = kh[j];

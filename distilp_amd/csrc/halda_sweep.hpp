@@ -72,7 +72,16 @@ __device__ inline DevFields load_fields(const halda_fleets &F, int64_t g) {
     return f;
 }
 
-__device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) {
+// The model as the sweep kernels see it: halda_model plus the uniform quotient (b_in / V) + b_out
+// formed once on the host (the same IEEE double operations, -ffp-contract=off: the same bits) instead
+// of by every wave.
+struct SweepModel : halda_model {
+    double bvo;  // (b_in / V) + b_out
+};
+
+__host__ __device__ inline double model_bvo(const halda_model &Mo) { return (Mo.b_in / Mo.V) + Mo.b_out; }
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F, double bvo) {
     DevCoef o;
     const double bp = Mo.b_prime;
     const int fl = F.flags;
@@ -87,7 +96,7 @@ __device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) {
     o.b = cls == 1 ? 0.0 : beta;
     o.xi = (F.r2v + F.v2r) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
     const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-    o.bcio = ((Mo.b_in / Mo.V) + Mo.b_out) * head + double(F.ccpu);
+    o.bcio = bvo * head + double(F.ccpu);
     const double sd = fmax(1.0, F.sdisk);
     o.p_bp = bp / sd;
     o.p_b = Mo.b_layer / sd;
@@ -95,6 +104,8 @@ __device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) {
     o.cst = o.xi + F.tcomm;
     return o;
 }
+
+__device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F) { return dev_coef(Mo, F, model_bvo(Mo)); }
 
 __device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F, int64_t g) {
     return dev_coef(Mo, load_fields(F, g));
@@ -634,9 +645,9 @@ __device__ inline double least_cycle(const FieldRec &r, int w, int n, const int 
     return Q >= P ? 0.5 * (P + Q) : P;
 }
 
-__device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, int &bad) {
+__device__ inline FieldRec field_rec(const SweepModel &Mo, const DevFields &F, int &bad) {
     FieldRec r;
-    const DevCoef c = dev_coef(Mo, F);
+    const DevCoef c = dev_coef(Mo, F, Mo.bvo);
     const double bp = Mo.b_prime;
     const int fl = F.flags;
     r.alpha = c.alpha; r.b = c.b; r.p_bp = c.p_bp; r.p_b = c.p_b; r.cst = c.cst;
@@ -677,7 +688,7 @@ __device__ inline FieldRec field_rec(const halda_model &Mo, const DevFields &F, 
 // load() runs on every lane (uniform control flow: the shuffles read every lane's registers).
 struct FieldSrc {
     using Rec = FieldRec;
-    const halda_model *Mo;
+    const SweepModel *Mo;
     const halda_fleets *F;
     const FieldRec *me;  // lane's own record (M <= lanes per problem), or nullptr
     int64_t d0;
@@ -711,7 +722,7 @@ __device__ inline double kappa_head(const halda_model &Mo, int flags, double scp
 }
 
 template <class SG>
-__device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
+__device__ inline void fleet_offsets_regs(const SweepModel &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
                                           double &xsum, double &kappa) {
     const bool act = sg.sl < M;
     // one wave sum for the three per-device constants of obj_value (t_comm, xi and kappa's tail term,
@@ -726,9 +737,8 @@ __device__ inline void fleet_offsets_regs(const halda_model &Mo, const DevFields
     // its order
     const int hf = sg.bcast(mf.flags, hi);
     const double scpu = sg.bcast(mf.scpu, hi), Tc = sg.bcast(mf.Tc, hi), sdisk = sg.bcast(mf.sdisk, hi);
-    const double bv = Mo.b_in / Mo.V;
     const int j = sg.sl & 3;
-    const double num = j == 0 ? Mo.f_out_b1 : j == 1 ? bv + Mo.b_out : j == 2 ? Mo.b_in : Mo.b_out;
+    const double num = j == 0 ? Mo.f_out_b1 : j == 1 ? Mo.bvo : j == 2 ? Mo.b_in : Mo.b_out;
     const double den = j == 0 ? scpu : j == 1 ? Tc : j == 2 ? Mo.V * sdisk : sdisk;
     const double q = num / den;
     const double q0 = sg.bcast(q, 0), q1 = sg.bcast(q, 1), q2 = sg.bcast(q, 2), q3 = sg.bcast(q, 3);
@@ -796,7 +806,7 @@ struct FleetOut {
 constexpr int kOutObk = 1, kOutSt = 2, kOutX = 4, kOutC = 8, kOutXC = kOutX | kOutC, kOutXZ = 16;
 
 struct SweepArgs {
-    halda_model Mo;
+    SweepModel Mo;
     halda_fleets F;
     int n_k;
     int uM;                        // > 0: every fleet has uM devices (dev_off[f] = dev_off[0] + f uM)
@@ -866,7 +876,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     constexpr bool kSeg = S < 64;
     constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
     const int lane = sg.sl;  // device index within the fleet
-    const halda_model &Mo = A.Mo;
+    const SweepModel &Mo = A.Mo;
     const halda_fleets &F = A.F;
     HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
@@ -916,6 +926,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     }
     bad = sg.any(bad != 0) ? 1 : 0;
     HALDA_SSTAMP(1, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_EXIT_AT) && HALDA_EXIT_AT == 1  // diagnostic: VALU of the records phase alone
+    if constexpr (!kTables && !kSeg) {
+        const double sink = me.alpha + me.b + me.p_bp + me.p_b + me.cst + double(me.Kset + me.Kvram + me.cls + me.gpu) +
+                            tsum + xsum + kappa + double(bad);
+        if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+        return;
+    }
+#endif
     HALDA_SSTAMP(9, __builtin_amdgcn_s_memrealtime());
     double best = kInf;
     int best_k = 0;
@@ -971,6 +989,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             bool haveE = true;  // gE / nE hold the split at w = 1 + e (k1_alloc), else split here
             me.W = W;
             if (k == 1) HALDA_SSTAMP(2, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_EXIT_AT) && HALDA_EXIT_AT == 2  // diagnostic: records + the bookkeeping before the greedy
+            if constexpr (!kTables && !kSeg) {
+                const double sink = me.alpha + me.b + me.p_bp + me.p_b + me.cst + double(me.Kset + me.Kvram + me.cls +
+                                    me.gpu + me.W + k + W) + tsum + xsum + kappa;
+                if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+                return;
+            }
+#endif
             // k = 1: the register greedy; W = M (R = 0): every w_i = 1 is forced, so the same code gives
             // the solution for any k (the output adds (k - 1) max_i H_i)
             if ((k == 1 || W == M) && regs && (!kTables || HALDA_SWEEP_TABLE_K1 || W == M)) {
@@ -986,6 +1012,13 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 }
             }
             if (k == 1) HALDA_SSTAMP(3, __builtin_amdgcn_s_memtime());
+#if defined(HALDA_EXIT_AT) && HALDA_EXIT_AT == 3  // diagnostic: ... + the k = 1 greedy
+            if constexpr (!kTables && !kSeg) {
+                const double sink = gE + double(e + nE + rounds + rc) + tsum + xsum + kappa;
+                if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+                return;
+            }
+#endif
             if (rc == K1_INFEASIBLE) {
                 st = HALDA_STATUS_INFEASIBLE;
             } else if (rc == K1_OK) {
