@@ -76,19 +76,36 @@ static int rate(PyObject *table, PyObject *Q, int fq, int *present, double *v) {
 /* ---------------------------------------------------------------- fast (parallel) pass
  * Large tables are packed by several threads while the calling thread holds the GIL and waits (small
  * ones by the calling thread itself), so
- * no Python code runs and no object changes meanwhile. The calling thread first collects every
- * device's instance dict (_PyObject_GetDictPtr, which on CPython 3.11+ may create the dict of an
- * object whose attributes are still inline: that happens there, under the GIL, never in a worker; an
- * object without an exact str-keyed dict sends the table to the serial pass). The workers only READ:
- * those borrowed dicts, lookups by precomputed hash in str-keyed dicts
+ * no Python code runs and no object changes meanwhile. Each device's instance dict: on CPython < 3.11
+ * _PyObject_GetDictPtr is pointer arithmetic on the object (tp_dictoffset), so the workers take it
+ * themselves; from 3.11 on it may create the dict of an object whose attributes are still inline (a
+ * managed dict), so there the calling thread collects every dict first, under the GIL (an object
+ * without an exact str-keyed dict sends the table to the serial pass). The workers only READ:
+ * the borrowed dicts, lookups by precomputed hash in str-keyed dicts
  * (_PyDict_GetItem_KnownHash: no error state, no Python code), and the values of exact float / int /
  * bool / None / str / dict objects. No reference count changes, no allocation, no exception: any
  * value outside that (a missing key, another type, an overflow, a FLOPs table without "b_1") makes the
  * worker give up, and the whole table is packed again by the serial pass below, which raises the
  * reference's exceptions in the reference's order. So the parallel pass either writes exactly what
  * the serial one would, or nothing that is kept. */
+#if PY_VERSION_HEX >= 0x030B0000
+#define DICTS_ON_CALLER 1 /* devs[] holds the instance dicts, collected by the calling thread */
+#else
+#define DICTS_ON_CALLER 0 /* devs[] holds the objects; a worker takes each one's dict (no allocation) */
+#endif
+
+/* the instance dict of entry g of devs[] (NULL: none, or not an exact str-keyed dict) */
+static PyObject *dev_dict(PyObject *o) {
+#if DICTS_ON_CALLER
+    return o;
+#else
+    PyObject **dp = _PyObject_GetDictPtr(o);
+    return dp && *dp && PyDict_CheckExact(*dp) ? *dp : NULL;
+#endif
+}
+
 typedef struct {
-    PyObject **devs; /* the devices' instance dicts */
+    PyObject **devs; /* the devices' instance dicts (DICTS_ON_CALLER) or objects */
     Py_ssize_t lo, hi, nd;
     PyObject *Q;
     Py_hash_t hQ;
@@ -232,9 +249,20 @@ static void prefetch_values(PyObject *d) {
 static void *worker(void *arg) {
     const Job *J = (const Job *)arg;
     for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g) {
-        if (g + PF_FAR < J->hi) __builtin_prefetch(J->devs[g + PF_FAR]);
-        if (g + PF_NEAR < J->hi) prefetch_values(J->devs[g + PF_NEAR]);
-        if (fast_dev(J, J->devs[g], g)) *J->bail = 1;
+        if (g + PF_FAR < J->hi) {
+            PyObject *o = J->devs[g + PF_FAR];
+            __builtin_prefetch(o);
+#if !DICTS_ON_CALLER
+            PyObject **dp = _PyObject_GetDictPtr(o);
+            if (dp) __builtin_prefetch(dp);
+#endif
+        }
+        if (g + PF_NEAR < J->hi) {
+            PyObject *d = dev_dict(J->devs[g + PF_NEAR]);
+            if (d) prefetch_values(d);
+        }
+        PyObject *d = dev_dict(J->devs[g]);
+        if (!d || !fdict(d) || fast_dev(J, d, g)) *J->bail = 1;
     }
     return NULL;
 }
@@ -269,10 +297,14 @@ static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f
         if (M == 0 || g + M > nd) { free(devs); return 0; }
         PyObject **items = PySequence_Fast_ITEMS(fl);
         for (Py_ssize_t i = 0; i < M; ++i) {
+#if DICTS_ON_CALLER
             if (i + PF_FAR < M) __builtin_prefetch(items[i + PF_FAR]);
-            PyObject **dp = _PyObject_GetDictPtr(items[i]); /* under the GIL: may create the dict (3.11+) */
+            PyObject **dp = _PyObject_GetDictPtr(items[i]); /* under the GIL: may create the dict */
             if (!dp || !*dp || !fdict(*dp)) { free(devs); return 0; }
             devs[g + i] = *dp;
+#else
+            devs[g + i] = items[i];
+#endif
         }
         g += M;
         off[f + 1] = g;
