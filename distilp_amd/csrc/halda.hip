@@ -444,6 +444,22 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
         }
         SA.n_parts = used + 1;
     }
+    // the leaf checks of an optimistic part 1 (kslot_check): the table slot with the smallest tables
+    // other than the split one (it ends its own solve first), else the other no-table slot, else the
+    // helper itself
+    SA.check_wave = -1;
+    if (SA.helper >= 0) {
+        SA.check_wave = SA.part_wave[0];
+        int best = 1 << 30;
+        for (int q = 0; q < SA.n_slot; ++q) {
+            if (q == SA.helper || q == SA.part_wave[0]) continue;
+            const int work = SA.tab[q] > 0 ? SA.r1[q] : (1 << 20);  // a no-table slot: its k = 1 greedy
+            if (work < best) {
+                best = work;
+                SA.check_wave = q;
+            }
+        }
+    }
     SA.crit_w4 = c->kslot_crit_w4;
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
@@ -1003,6 +1019,12 @@ int halda_debug_stamps(unsigned long long *out, int n_inst) {
     const int n = std::min(n_inst, kStampInst);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halda_stamps), sizeof(unsigned long long) * kStamps * n));
+    return n;
+}
+int halda_debug_scanprof(unsigned long long *out, int n_wave) {
+    const int n = std::min(n_wave, kStampInst);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halda_scanprof), sizeof(unsigned long long) * kScanProf * n));
     return n;
 }
 int halda_debug_dump(double *out) {

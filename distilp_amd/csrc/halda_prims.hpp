@@ -23,6 +23,10 @@ __device__ unsigned long long g_halda_stamps[kStampInst * kStamps];
 // the k = 2 tables G / H of the k-slot kernel's fleets (tools/kslot_tables.py): [fleet][device][e]
 constexpr int kDumpFleets = 4096, kDumpDev = 16, kDumpE = 32;
 __device__ double g_halda_dump[kDumpFleets * kDumpDev * kDumpE * 2];
+// the k-slot kernel's split-scan part 1: per (workgroup, slot) wave, shader cycles summed over the
+// threshold scan's iterations per step of an event (tools/scan_prof.py)
+constexpr int kScanProf = 64;  // 4 segments x 16
+__device__ unsigned long long g_halda_scanprof[kStampInst * kScanProf];
 #define HALDA_STAMP(k)                                                                                  \
     do {                                                                                                \
         if (lane == 0 && I.inst < kStampInst) g_halda_stamps[I.inst * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \

@@ -1001,6 +1001,7 @@ struct SplitArea {  // per segment, in LDS
     double s_inf, best0;
     int lo_sum, capsum;
     int pub;             // 0: not yet, 1: published, 2: part 1 does not scan (the helpers skip)
+    int verdict;         // the helper's leaf check of part 1's rows (optimistic part 1): 0 not yet, 1 ok, 2 not
     int lo[16], hi[16];  // each device's finite leaf range
     // the helpers -> part 1
     double alt_best[kMaxSplitParts - 1];  // part p's best objective (+inf: nothing beat its start)
@@ -1011,6 +1012,9 @@ struct ScanSplit {
     int part = 0;     // 0: no split, 1: the slot's own wave, 2: the helper
     int n_parts = 0;  // 2 (split) or 0
     SplitArea *ar = nullptr;
+#ifdef HALDA_STAMPS
+    unsigned long long *prof = nullptr;  // g_halda_scanprof of this wave (part 1 only)
+#endif
 };
 
 // Rank of v among the 16 lanes of its DPP row (ties: the lower lane first).
@@ -1025,6 +1029,22 @@ __device__ inline int rank16(double v, int sl, std::integer_sequence<int, R...>)
     return (rank_step<R + 1>(v, sl) + ...);
 }
 
+// Largest cap in [cap, hi] with H[cap] <= T, H nondecreasing on the row's finite range (checked by the
+// leaf scan): eight entries per LDS round trip (the entries <= T are a prefix of each chunk).
+__device__ inline int advance_cap(const double *H, int cap, int hi, double T) {
+    while (cap < hi) {
+        double hv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) hv[t] = H[min(cap + 1 + t, hi)];
+        int adv = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) adv += (cap + 1 + t <= hi && hv[t] <= T) ? 1 : 0;
+        cap += adv;
+        if (adv < 8) break;
+    }
+    return cap;
+}
+
 template <class SG>
 __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &sg, double s_inf, double best0,
                                     int64_t &nodes, const LeafInfo &li0, const ScanSplit sp = ScanSplit{}) {
@@ -1033,6 +1053,18 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     const int lane = sg.sl;  // device index within the problem
     if (M > SG::S || M < 2 || !li0.convex || !li0.mono || li0.empty) return false;
     HALDA_KSTAMP(3);
+#ifdef HALDA_STAMPS  // diagnostic build: cycles per step, summed over the events (tools/scan_prof.py)
+    unsigned long long pa[12] = {}, tp = __builtin_amdgcn_s_memtime();
+#define HALDA_SCANPROF(slot, ...)                                        \
+    do {                                                                 \
+        asm volatile("" ::__VA_ARGS__);                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
+        pa[slot] += t_ - tp;                                             \
+        tp = t_;                                                         \
+    } while (0)
+#else
+#define HALDA_SCANPROF(slot, ...) do {} while (0)
+#endif
     const bool act = lane < M;
     const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
     const int lo = act ? li0.my_lo : 0, hi = act ? li0.my_hi : -1;
@@ -1040,9 +1072,8 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     if (need_total < 0 || need_total > li0.cap) return false;
     // start at T0 = max_i H_i(lo_i): every device can sit at its first allowed e
     double T = sg.max_f64(act ? H[lo] : -kInf);
-    int cap = lo;
-    if (act)
-        while (cap < hi && H[cap + 1] <= T) ++cap;
+    int cap = act ? advance_cap(H, lo, hi, T) : lo;
+    HALDA_SCANPROF(5, "v"(cap), "v"(T));
     const int part = sp.part;
     double t_stop = kInf;  // the part's upper cut (inclusive)
     if constexpr (SG::S == 16) {
@@ -1056,11 +1087,11 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             t_stop = part == 1 ? ta : kInf;
             if (part > 1) {
                 T = ta;
-                if (act)
-                    while (cap < hi && H[cap + 1] <= T) ++cap;
+                if (act) cap = advance_cap(H, cap, hi, T);
             }
         }
     }
+    HALDA_SCANPROF(6, "v"(cap), "v"(T), "v"(t_stop));
     // optimal capped allocation at T0 (a helper: at its lower cut) (greedy: every cap filled from lo, then the smallest increments)
     int e = lo;
     int need = need_total;
@@ -1084,6 +1115,7 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             }
         }
     }
+    HALDA_SCANPROF(7, "v"(e), "v"(need));
     double S = sg.sum_f64(act ? G[e] : 0.0);
     HALDA_KSTAMP(4);
     double best = best0;
@@ -1102,9 +1134,16 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     // decreases: such an opening is taken at the current T (its H is <= T, so it is allowed there), and
     // the recorded kc T + S stays the cost of an allocation whose cycle times are all <= T. The
     // exchanges it allows change S by rounding only.
-    double hn = act && cap < hi ? H[cap + 1] : kInf;   // H of this device's next cap
+    // Per lane, in registers: the next two openings (cap + 1, cap + 2: H and the unit each opens) and the
+    // last two taken units (at e, e - 1), so that an event moves its two lanes by register shifts; the
+    // LDS reads that refill the shifted-out entry are issued during the event and first used at a later
+    // one. Every value is the one the reads at the event would give (the same two-entry differences).
+    double hn = act && cap < hi ? H[cap + 1] : kInf;           // H of this device's next cap
     double gn = act && cap < hi ? G[cap + 1] - G[cap] : kInf;  // the unit it opens (cap -> cap + 1)
-    double lt = act && e > lo ? G[e] - G[e - 1] : -kInf;  // its last taken unit
+    double hn2 = act && cap + 1 < hi ? H[cap + 2] : kInf;      // the same one cap further
+    double gn2 = act && cap + 1 < hi ? G[cap + 2] - G[cap + 1] : kInf;
+    double lt = act && e > lo ? G[e] - G[e - 1] : -kInf;       // its last taken unit
+    double lt2 = act && e - 1 > lo ? G[e - 1] - G[e - 2] : -kInf;  // the one below it
     double lam = -kInf;
     int lj = -1;
     if (need == 0) {
@@ -1116,45 +1155,62 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             bestE = part > 1 ? -1 : e;
         }
     }
+    HALDA_SCANPROF(8, "v"(S), "v"(lam), "v"(hn), "v"(gn), "v"(lt), "v"(best));
     while (true) {
-        const bool useful = act && e == cap && cap < hi && (need > 0 || gn < lam);
+        // useful: at its cap, with a next cap (else hn = gn = +inf), and needed or beating lam
+        const double lamU = need > 0 ? kInf : lam;
+        const bool useful = (e == cap) & (gn < lamU);  // (no short circuit: one select, no branch)
         const double cand = useful ? hn : kInf;
         const double Tn = sg.min_f64(cand);
-        const double Te = fmax(T, Tn);  // (+inf when no opening is left)
+        const double Te = vmax_f64(T, Tn);  // (+inf when no opening is left)
         if (!(Tn < kInf) || !(kc * Te + s_inf < best) || Te > t_stop) break;
+        HALDA_SCANPROF(0, "v"(Te));
         const int li = sg.lowest(cand == Tn);
         ++events;
         const double d = sg.bcast(gn, li);
+        HALDA_SCANPROF(1, "v"(d));
         const bool swap = need == 0;  // else: fill
-        const int ljo = lj;
+        // li takes the unit its new cap opens; lj gives back its largest taken unit (li == lj only
+        // through the convexity tolerance: then both, e unchanged)
+        const bool is_li = lane == li, is_lj = swap && lane == lj;
+        const int cap_n = is_li ? cap + 1 : cap;
+        const int e_n = is_li ? (is_lj ? e : e + 1) : (is_lj ? e - 1 : e);
+        const double lt_n = is_li ? (is_lj ? lt : gn) : (is_lj ? lt2 : lt);
+        double lt2_n = is_li && !is_lj ? lt : lt2;
+        // refills: li's opening at cap_n + 1, lj's unit at e_n - 1 (clamped reads on every lane)
+        const bool rj = is_lj && !is_li;
+        const int ia = is_li ? min(cap_n + 2, hi) : max(e_n - 1, 0);
+        const int ib = is_li ? min(cap_n + 1, hi) : max(e_n - 2, 0);
+        const double r0 = G[ia], r1 = G[ib], r2 = H[ia];
+        if (is_li) {
+            hn = hn2;
+            gn = gn2;
+        }
+        hn2 = is_li ? (cap_n + 1 < hi ? r2 : kInf) : hn2;
+        gn2 = is_li ? (cap_n + 1 < hi ? r0 - r1 : kInf) : gn2;
+        lt2_n = rj ? (e_n - 1 > lo ? r0 - r1 : -kInf) : lt2_n;
+        cap = cap_n;
+        e = e_n;
+        lt = lt_n;
+        lt2 = lt2_n;
+        HALDA_SCANPROF(2, "v"(lt), "v"(gn), "v"(e));
+        // lam after the event (its reduction needs no LDS value: it overlaps the broadcast of d)
+        const int need_n = swap ? 0 : need - 1;
+        const double lam_n = sg.max_f64(lt_n);
+        const int lj_n = sg.highest(lt_n == lam_n);
+        HALDA_SCANPROF(3, "v"(lam_n), "v"(lj_n));
         S += swap ? d - lam : d;
-        if (!swap) --need;
-        // li takes the unit its new cap opens; ljo gives back its largest taken unit (li == ljo only
-        // through the convexity tolerance: then in that order). All LDS reads in one round trip.
-        const bool is_li = lane == li, is_lj = swap && lane == ljo;
-        if (is_li || is_lj) {
-            const int ncap = is_li ? e + 1 : cap;
-            const int ne = is_li ? (is_lj ? e : e + 1) : e - 1;
-            const int a = min(ncap + 1, hi), b = max(ne - 1, 0);
-            const double Gn1 = G[a], Gn0 = G[ncap], Hn1 = H[a], Ge = G[ne], Gm = G[b];
-            if (is_li) {
-                cap = ncap;
-                hn = cap < hi ? Hn1 : kInf;
-                gn = cap < hi ? Gn1 - Gn0 : kInf;
-            }
-            e = ne;
-            lt = is_lj ? (e > lo ? Ge - Gm : -kInf) : Ge - Gm;
-        }
-        if (need == 0) {
-            lam = sg.max_f64(lt);
-            lj = sg.highest(lt == lam);
-        }
+        need = need_n;
+        lam = need_n == 0 ? lam_n : -kInf;
+        lj = need_n == 0 ? lj_n : -1;
         T = Te;
-        if (need == 0 && kc * T + S < best) {
-            best = kc * T + S;
-            bestE = e;
-        }
+        const double v = kc * T + S;
+        const bool imp = (need == 0) & (v < best);
+        best = imp ? v : best;
+        bestE = imp ? e : bestE;
+        HALDA_SCANPROF(4, "v"(best), "v"(bestE));
     }
+    HALDA_SCANPROF(9, "v"(best));
     nodes += events;
     HALDA_KSTAMP(5);
     if constexpr (SG::S == 16) {
@@ -1178,11 +1234,80 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             }
         }
     }
+    HALDA_SCANPROF(10, "v"(best), "v"(bestE));
+#ifdef HALDA_STAMPS
+    if (sp.prof && lane == 0 && act) {
+        unsigned long long *o = sp.prof + 16 * (sg.base / 16);
+        for (int t = 0; t < 11; ++t) o[t] = pa[t];
+        o[15] = (unsigned long long)events;
+    }
+#endif
+#undef HALDA_SCANPROF
     if (bestE >= 0) {  // a capped optimum beat the unconstrained allocation's own T
         if (act) w.st0[lane] = bestE;
     }
     wave_sync();
     return true;
+}
+
+// The leaf checks of one row (lane = device): its finite range [lo, hi] (cnt entries), G convex on it
+// within the 1e-12 tolerance (ok), H nondecreasing on it (mono). The caller's lo / hi / cnt / ok / mono
+// start at R1 / -1 / 0 / true / true.
+__device__ inline void leaf_scan(const double *G, const double *H, int R1, bool act, int &lo, int &hi, int &cnt,
+                                 bool &ok, bool &mono) {
+    // The row in chunks of 8 entries, the next chunk's 16 LDS reads issued before this chunk is
+    // checked (one LDS latency for the whole row, not one per entry). No chain between entries: each
+    // entry is checked against its two predecessors (g1, g2; d1 = g1 - g2), which in a contiguous
+    // finite range are the sequential scan's prev / dprev, bit for bit; a gap in the range fails the
+    // contiguity test at the end, as the sequential scan's "hi == e - 1" fails at the entry after it.
+    if (act) {
+        double gc[8], hc[8];
+        auto load = [&](int e0, double (&g)[8], double (&h)[8]) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int e = min(e0 + t, R1 - 1);
+                g[t] = G[e];
+                h[t] = H[e];
+            }
+        };
+        load(0, gc, hc);
+        double g1 = kInf, d1 = -kInf, h1 = -kInf;
+        bool f1 = false, f2 = false;
+        for (int e0 = 0; e0 < R1; e0 += 8) {
+            double gx[8], hx[8];
+            load(e0 + 8, gx, hx);  // the next chunk (clamped: in the row)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int e = e0 + t;
+                const double g = gc[t], h = hc[t];
+                const bool fin = e < R1 && g < kInf;
+                const double d = g - g1;
+                const bool conv = !(fin && f1 && f2) || d >= d1 - 1e-12 * fmax(1.0, fabs(g));
+                ok = ok && conv;
+                mono = mono && (!fin || h >= (f1 ? h1 : -kInf));
+                lo = fin ? min(lo, e) : lo;
+                hi = fin ? e : hi;
+                cnt += fin ? 1 : 0;
+                g1 = g;
+                d1 = d;
+                h1 = h;
+                f2 = f1;
+                f1 = fin;
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                gc[t] = gx[t];
+                hc[t] = hx[t];
+            }
+        }
+        ok = ok && (cnt == 0 || cnt == hi - lo + 1);
+    }
+}
+
+// Every device of the segment has a finite first and last entry (segment-uniform).
+template <class SG>
+__device__ inline bool leaf_ends_finite(const double *G, int R1, bool act, const SG &sg) {
+    return !sg.any(act && !(G[0] < kInf && G[R1 - 1] < kInf));
 }
 
 // k > 1 for fleets of at most 64 devices with convex leaves and nondecreasing cycle times (every
@@ -1196,41 +1321,44 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const int lane = sg.sl;
     const bool act = lane < M;
+#ifdef HALDA_STAMPS  // diagnostic build (tools/scan_prof.py): entry time, leaf scan, checks, phase 0
+    unsigned long long lp_t0 = __builtin_amdgcn_s_memtime(), lp_t1 = 0, lp_t2 = 0, lp_t3 = 0;
+#endif
     const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
     int lo = R1, hi = -1, cnt = 0;
     bool ok = true, mono = true;
-    double prev = kInf, dprev = -kInf, hprev = -kInf;
-    // the row in chunks of 8 entries: the chunk's 16 LDS reads are issued together, then the entries
-    // are scanned in registers with selects (one LDS round trip per chunk, not per entry)
-    if (act)
-        for (int e0 = 0; e0 < R1; e0 += 8) {
-            double gc[8], hc[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const int e = min(e0 + t, R1 - 1);
-                gc[t] = G[e];
-                hc[t] = H[e];
-            }
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const int e = e0 + t;
-                const double g = gc[t], h = hc[t];
-                const bool fin = e < R1 && g < kInf;
-                const double d = g - prev;
-                const bool conv = (hi == e - 1) && d >= dprev - 1e-12 * fmax(1.0, fabs(g));
-                ok = (fin && cnt > 0) ? ok && conv : ok;
-                dprev = (fin && cnt > 0) ? d : dprev;
-                mono = fin ? mono && h >= hprev : mono;
-                hprev = fin ? h : hprev;
-                lo = fin ? min(lo, e) : lo;
-                hi = fin ? e : hi;
-                prev = fin ? g : prev;
-                cnt += fin ? 1 : 0;
+    // part 1 of a split scan whose rows are finite at both ends takes them as [0, R1 - 1] and goes on
+    // at once; the helper wave checks them meanwhile (kslot_helper), and the verdict is awaited before
+    // this returns (a failed check returns -1, as the check here would have)
+    const bool opt = sp.part == 1 && leaf_ends_finite(G, R1, act, sg);
+    if (opt) {
+        if (act) {
+            lo = 0;
+            hi = R1 - 1;
+            cnt = R1;
+        }
+    } else {
+        leaf_scan(G, H, R1, act, lo, hi, cnt, ok, mono);
+    }
+    auto done = [&](int r) {  // an optimistic part 1 returns the helper's verdict on its rows first
+        if constexpr (SG::S == 16) {
+            if (opt) {
+                while (sg.any(__hip_atomic_load(&sp.ar->verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0))
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (sp.ar->verdict != 1) return -1;
             }
         }
+        return r;
+    };
+#ifdef HALDA_STAMPS
+    asm volatile("" ::"v"(ok), "v"(mono), "v"(cnt), "v"(lo), "v"(hi));
+    lp_t1 = __builtin_amdgcn_s_memtime();
+#endif
     if (sg.any(act && (!ok || !mono))) return -1;
     if (sg.any(act && cnt == 0)) return 0;
 #ifdef HALDA_STAMPS
+    lp_t2 = __builtin_amdgcn_s_memtime();
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();  // leaf scan done
 #else
     (void)stamp;
@@ -1244,7 +1372,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     li.my_lo = act ? lo : 0;
     li.my_hi = act ? hi : -1;
     int need = (R1 - 1) - li.lo_sum;
-    if (need < 0 || need > li.cap) return 0;
+    if (need < 0 || need > li.cap) return done(0);
     // phase 0: unconstrained greedy exchange (rounds: the smallest next increment wins and keeps
     // every one still beating the runner-up)
     int e = act ? lo : 0;
@@ -1262,6 +1390,17 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
         }
         need -= t;
     }
+#ifdef HALDA_STAMPS
+    asm volatile("" ::"v"(e));
+    lp_t3 = __builtin_amdgcn_s_memtime();
+    if (sp.prof && lane == 0 && act) {
+        unsigned long long *o = sp.prof + 16 * (sg.base / 16);
+        o[11] = lp_t1 - lp_t0;
+        o[12] = lp_t2 - lp_t1;
+        o[13] = lp_t3 - lp_t2;
+        o[14] = lp_t0;
+    }
+#endif
     const double s_inf = sg.sum_f64(act ? G[e] : 0.0);
     const double hmax = sg.max_f64(act ? fmax(0.0, H[e]) : 0.0);
     if (act) w.st0[lane] = e;
@@ -1285,7 +1424,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     }
     kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li, sp);
     wave_sync();
-    return 1;
+    return done(1);
 }
 
 // DP pass; k > 1: ascending threshold scan with bound pruning. One tree_dp call

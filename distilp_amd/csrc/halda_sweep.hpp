@@ -1349,6 +1349,7 @@ struct SlotArgs {
     int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
     int rec_off;               // LDS byte offset of the workgroup's device records (KslotRecs)
+    int check_wave;            // the wave that checks the split slot's leaves after its own slot (-1: none)
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
 };
 static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
@@ -1687,6 +1688,27 @@ __device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const 
     }
 }
 
+// The leaf checks of the split slot's rows for an optimistic part 1 (dp_pass_lanes takes rows finite at
+// both ends as [0, R1 - 1] without checking them and awaits this verdict before it returns): made by
+// SA.check_wave after its own slot, the wave whose slot ends first, while part 1 scans.
+__device__ void kslot_check(const SweepArgs &A, const SlotArgs &SA, const KslotFleet &fd, SplitArea *ar,
+                            const Seg<kSegLanes> &sg, unsigned char *smem, int seg, bool live) {
+    const int p = SA.helper, lane = sg.sl;
+    const int j = SA.j[p], k = A.ks[j], W = A.Ws[j];
+    if (!live || !kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) return;
+    const int M = fd.M, R1 = W - M + 1, RS = odd_stride(R1);
+    const bool act = lane < M;
+    const WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
+    const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
+    if (!leaf_ends_finite(G, R1, act, sg)) return;  // part 1 checks these itself
+    int lo = R1, hi = -1, cnt = 0;
+    bool ok = true, mono = true;
+    leaf_scan(G, H, R1, act, lo, hi, cnt, ok, mono);
+    const int v = sg.any(act && (!ok || !mono)) ? 2 : 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&ar->verdict, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // A helper wave of a k-slot workgroup, after its own slot: its part (T range) of the split slot's
 // threshold scan for its segment's fleet, from what part 1 published after its leaf scan and phase-0
 // greedy (part 1 publishes on every path: "skip" when it does not scan), into the split area; then
@@ -1788,18 +1810,22 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         if (f < nf) kslot_tables(A, SA, q, crit, fd, sg, smem, seg);
         const int my_part = kslot_part_of(SA, q);
         if (my_part && sg.sl == 0) split->flag[my_part - 2] = 0;  // posted after the barrier
-        if (q == SA.helper && sg.sl == 0) split->pub = 0;
+        if (q == SA.helper && sg.sl == 0) {
+            split->pub = 0;
+            split->verdict = 0;
+        }
         HALDA_KSTAMPW(6, __builtin_amdgcn_s_memtime());
         __syncthreads();  // every slot's tables are complete
         HALDA_KSTAMPW(11, __builtin_amdgcn_s_memtime());
         if (q == SA.n_slot) {  // an extra helper wave: no slot of its own
             __builtin_amdgcn_s_setprio(3);
+            if (q == SA.check_wave) kslot_check(A, SA, fd, split, sg, smem, seg, f < nf);
             kslot_helper(A, SA, fd, split, my_part, sg, smem, seg, f < nf);
             __syncthreads();  // the pick barrier below
             return;
         }
         const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
-#ifdef HALDA_STAMPS
+#ifdef HALDA_STAMPS_DUMP  // (-DHALDA_STAMPS -DHALDA_STAMPS_DUMP: tools/kslot_tables.py)
         if (f < kDumpFleets && A.ks[SA.j[q]] == 2 && SA.tab[q] > 0 && lane % kSegLanes < fd.M) {
             const int R1 = A.Ws[SA.j[q]] - fd.M + 1, RS = odd_stride(R1), i = lane % kSegLanes;
             for (int e = 0; e < kDumpE; ++e) {
@@ -1810,10 +1836,18 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         }
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
+#ifdef HALDA_STAMPS
+        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split,
+                           int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
+                               ? g_halda_scanprof + (int64_t(blockIdx.x) * SA.n_slot + q) * kScanProf
+                               : nullptr};
+#else
         const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split};
+#endif
         if (f < nf)
             sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
         if (q == SA.helper && f < nf && sg.sl == 0 && split->pub == 0) split->pub = 2;  // did not scan: helpers skip
+        if (q == SA.check_wave) kslot_check(A, SA, fd, split, sg, smem, seg, f < nf);
         if (my_part) {  // after its own slot, at the split slot's priority
             __builtin_amdgcn_s_setprio(3);
             kslot_helper(A, SA, fd, split, my_part, sg, smem, seg, f < nf);

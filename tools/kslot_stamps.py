@@ -65,6 +65,19 @@ def main():
     print(f"  pick (slot 0) {np.percentile(s0[:, 4] - s0[:, 3], q)}")
     life = st[:, :, 4].max(axis=1) - st[:, :, 0].min(axis=1)
     print(f"  workgroup life {np.percentile(life, q)}")
+    # the slowest workgroups (they set the launch): each slot wave's phases, and the k = 2 wave's steps
+    t0 = st[:, :, 0].min(axis=1)
+    for g in np.argsort(life)[-6:][::-1]:
+        parts = []
+        for j, k in enumerate(slots):
+            s = st[g, j] - t0[g]
+            parts.append(f"k={k}: rec {s[1]} tab {s[6]} bar {s[11]} solved {s[2]}")
+        line = f"  wg {g} life {life[g]}: " + " | ".join(parts)
+        if 2 in slots:
+            s = st[g, slots.index(2)]
+            line += (f" || k=2 leaf {s[9] - s[11]} ph0 {s[10] - s[9]} scan {s[7] - s[10]} ev {s[8]}"
+                     f" out {s[2] - s[7]}")
+        print(line)
     t0 = st[:, :, 5] & ((1 << 40) - 1)
     print(f"  wave start spread (10 ns ticks) {np.percentile(t0 - t0.min(), [0, 10, 50, 90, 100])}")
     hw = (st[:, :, 5] >> 40) & 0xFFFF  # HW_ID[15:0]: wave slot [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]

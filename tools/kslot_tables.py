@@ -1,6 +1,7 @@
 """Diagnostic: dump the k = 2 tables (G, H per device and layer count) the k-slot kernel builds for
-the C2 fleets, from a -DHALDA_STAMPS build, to gpurun_out/c2_tables.npz (offline study of the
-threshold scan).   HALDA_LIB=build/variants/libhalda_stamps.so python tools/kslot_tables.py"""
+the C2 fleets, from a -DHALDA_STAMPS -DHALDA_STAMPS_DUMP build (make -C distilp_amd/csrc dump), to
+gpurun_out/c2_tables.npz (offline study of the threshold scan).
+  HALDA_LIB=build/variants/libhalda_dump.so python tools/kslot_tables.py"""
 import ctypes
 import sys
 from pathlib import Path
