@@ -985,9 +985,9 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 //
 // Split over two waves of a k-slot workgroup (16-lane segments only, sp.part != 0): the scan's length
 // is the workgroup's critical path, and each event is a dependent chain of reductions, so the
-// candidate range is cut at T_a (the lower median over the devices of H at cap(T0) + 2;
-// tools/scan_model.py on dumped C2 tables: the longest scan per wave 47 -> 28 events) and the two
-// parts run at once. Part 1 (the slot's own wave) takes the openings T <= T_a; part 2 (a helper wave)
+// candidate range is cut at T_a (the value of rank 5/8 among the devices' H at cap(T0) + 2;
+// tools/scan_model.py on dumped C2 tables: the longest scan per wave 47 -> 28 events at the median) and
+// the two parts run at once. Part 1 (the slot's own wave) takes the openings T <= T_a; part 2 (a helper wave)
 // starts from an optimal capped allocation at T_a (the greedy's) and takes the openings above it,
 // pruning with its own bound. Under ties (repeated devices) that allocation need not be the one the
 // one scan holds at T_a, and it does not have to be: an exchange keeps ANY optimal capped allocation
@@ -1012,6 +1012,7 @@ struct ScanSplit {
     int part = 0;     // 0: no split, 1: the slot's own wave, 2: the helper
     int n_parts = 0;  // 2 (split) or 0
     SplitArea *ar = nullptr;
+    bool fetch = false;  // part 1: s_inf / best0 come from the helper's phase 0 (published in ar)
 #ifdef HALDA_STAMPS
     unsigned long long *prof = nullptr;  // g_halda_scanprof of this wave (part 1 only)
 #endif
@@ -1046,8 +1047,9 @@ __device__ inline int advance_cap(const double *H, int cap, int hi, double T) {
 }
 
 template <class SG>
-__device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &sg, double s_inf, double best0,
+__device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &sg, double s_inf_in, double best0_in,
                                     int64_t &nodes, const LeafInfo &li0, const ScanSplit sp = ScanSplit{}) {
+    double s_inf = s_inf_in, best0 = best0_in;
     const int M = I.M, R1 = I.R1, RS = I.RS;
     const double kc = I.kc;
     const int lane = sg.sl;  // device index within the problem
@@ -1083,7 +1085,9 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             const int n = sg.sum_i(has ? 1 : 0);
             const int r2 = rank16(v2, lane, std::make_integer_sequence<int, 15>{});
             // the cut (> T0; +inf: no opening at all)
-            const double ta = sg.min_f64(has && r2 == (n - 1) / 2 ? v2 : kInf);
+            // (rank 5/8 of the way up: part 1 leaves its leaf checks and phase 0 to other waves, so
+            // it takes the larger share of the range; measured against 4/8 and 6/8)
+            const double ta = sg.min_f64(has && r2 == (n - 1) * 5 / 8 ? v2 : kInf);
             t_stop = part == 1 ? ta : kInf;
             if (part > 1) {
                 T = ta;
@@ -1118,6 +1122,15 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     HALDA_SCANPROF(7, "v"(e), "v"(need));
     double S = sg.sum_f64(act ? G[e] : 0.0);
     HALDA_KSTAMP(4);
+    if constexpr (SG::S == 16) {
+        if (sp.part == 1 && sp.fetch) {  // the helper's phase 0 (its s_inf and bound), needed from here on
+            while (sg.any(__hip_atomic_load(&sp.ar->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0))
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            s_inf = sp.ar->s_inf;
+            best0 = sp.ar->best0;
+        }
+    }
     double best = best0;
     int bestE = -1;
     int64_t events = 0;
@@ -1250,6 +1263,45 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
     return true;
 }
 
+// Part 1's publication for the helpers of a split scan: the leaf ranges, phase 0's s_inf and bound.
+__device__ inline void split_publish(SplitArea *ar, int lane, bool act, int lo, int hi, double s_inf, double best0,
+                                     int lo_sum, int capsum) {
+    if (act) {
+        ar->lo[lane] = lo;
+        ar->hi[lane] = hi;
+    }
+    if (lane == 0) {
+        ar->s_inf = s_inf;
+        ar->best0 = best0;
+        ar->lo_sum = lo_sum;
+        ar->capsum = capsum;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&ar->pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Phase 0 of a k > 1 instance: the unconstrained greedy exchange from e = lo (rounds: the smallest next
+// increment wins and keeps every one still beating the runner-up); e ends at the allocation.
+template <class SG>
+__device__ inline void phase0_greedy(const double *Gall, int RS, int need, const SG &sg, bool act, int hi, int &e) {
+    const int lane = sg.sl;
+    const double *G = Gall + int64_t(act ? lane : 0) * RS;
+    double inc = act && e < hi ? G[e + 1] - G[e] : kInf;
+    while (need > 0) {
+        const double bv = sg.min_f64(inc);
+        const int win = sg.lowest(inc == bv);
+        const double rv = lane == win ? kInf : inc;
+        const double m2 = sg.min_f64(rv);
+        const int d2 = sg.lowest(rv == m2);
+        const int t = take_run(Gall + int64_t(win) * RS, sg.bcast(e, win), sg.bcast(hi, win), need, m2, win < d2, sg);
+        if (lane == win) {
+            e += t;
+            inc = e < hi ? G[e + 1] - G[e] : kInf;
+        }
+        need -= t;
+    }
+}
+
 // The leaf checks of one row (lane = device): its finite range [lo, hi] (cnt entries), G convex on it
 // within the 1e-12 tolerance (ok), H nondecreasing on it (mono). The caller's lo / hi / cnt / ok / mono
 // start at R1 / -1 / 0 / true / true.
@@ -1328,8 +1380,8 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     int lo = R1, hi = -1, cnt = 0;
     bool ok = true, mono = true;
     // part 1 of a split scan whose rows are finite at both ends takes them as [0, R1 - 1] and goes on
-    // at once; the helper wave checks them meanwhile (kslot_helper), and the verdict is awaited before
-    // this returns (a failed check returns -1, as the check here would have)
+    // at once: another wave checks them meanwhile (kslot_check) and the verdict is awaited before this
+    // returns (a failed check returns -1, as the check here would have); the helper makes phase 0
     const bool opt = sp.part == 1 && leaf_ends_finite(G, R1, act, sg);
     if (opt) {
         if (act) {
@@ -1373,54 +1425,48 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     li.my_hi = act ? hi : -1;
     int need = (R1 - 1) - li.lo_sum;
     if (need < 0 || need > li.cap) return done(0);
-    // phase 0: unconstrained greedy exchange (rounds: the smallest next increment wins and keeps
-    // every one still beating the runner-up)
-    int e = act ? lo : 0;
-    double inc = act && e < hi ? G[e + 1] - G[e] : kInf;
-    while (need > 0) {
-        const double bv = sg.min_f64(inc);
-        const int win = sg.lowest(inc == bv);
-        const double rv = lane == win ? kInf : inc;
-        const double m2 = sg.min_f64(rv);
-        const int d2 = sg.lowest(rv == m2);
-        const int t = take_run(w.G + int64_t(win) * RS, sg.bcast(e, win), sg.bcast(hi, win), need, m2, win < d2, sg);
-        if (lane == win) {
-            e += t;
-            inc = e < hi ? G[e + 1] - G[e] : kInf;
-        }
-        need -= t;
-    }
+    // phase 0: unconstrained greedy exchange -- by the helper wave for an optimistic part 1 (it publishes
+    // s_inf, the bound and the allocation in st0; the scan awaits them before its first event)
 #ifdef HALDA_STAMPS
-    asm volatile("" ::"v"(e));
-    lp_t3 = __builtin_amdgcn_s_memtime();
-    if (sp.prof && lane == 0 && act) {
-        unsigned long long *o = sp.prof + 16 * (sg.base / 16);
-        o[11] = lp_t1 - lp_t0;
-        o[12] = lp_t2 - lp_t1;
-        o[13] = lp_t3 - lp_t2;
-        o[14] = lp_t0;
-    }
+    auto prof_rec = [&]() {
+        lp_t3 = __builtin_amdgcn_s_memtime();
+        if (sp.prof && lane == 0 && act) {
+            unsigned long long *o = sp.prof + 16 * (sg.base / 16);
+            o[11] = lp_t1 - lp_t0;
+            o[12] = lp_t2 - lp_t1;
+            o[13] = lp_t3 - lp_t2;
+            o[14] = lp_t0;
+        }
+    };
 #endif
+    if (opt) {
+#ifdef HALDA_STAMPS
+        prof_rec();
+#endif
+        LeafInfo lf = li;
+        nodes = 1;
+        kc_scan_incremental(w, I, sg, 0.0, 0.0, nodes, lf, ScanSplit{sp.part, sp.n_parts, sp.ar, true
+#ifdef HALDA_STAMPS
+                                                                     , sp.prof
+#endif
+                                                                     });
+        wave_sync();
+        return done(1);
+    }
+    int e = act ? lo : 0;
+    phase0_greedy(w.G, RS, need, sg, act, hi, e);
     const double s_inf = sg.sum_f64(act ? G[e] : 0.0);
     const double hmax = sg.max_f64(act ? fmax(0.0, H[e]) : 0.0);
     if (act) w.st0[lane] = e;
     nodes = 1;
 #ifdef HALDA_STAMPS
+    asm volatile("" ::"v"(e));
+    prof_rec();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();  // phase-0 greedy done
 #endif
-    if (sp.part == 1) {  // the helpers start from here (kslot_helper)
-        if (act) {
-            sp.ar->lo[lane] = lo;
-            sp.ar->hi[lane] = hi;
-        }
-        if (lane == 0) {
-            sp.ar->s_inf = s_inf;
-            sp.ar->best0 = I.kc * hmax + s_inf;
-            sp.ar->lo_sum = li.lo_sum;
-            sp.ar->capsum = li.cap;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&sp.ar->pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (SG::S == 16) {
+        if (sp.part == 1)  // the helpers start from here (kslot_helper)
+            split_publish(sp.ar, lane, act, lo, hi, s_inf, I.kc * hmax + s_inf, li.lo_sum, li.cap);
     }
     kc_scan_incremental(w, I, sg, s_inf, I.kc * hmax + s_inf, nodes, li, sp);
     wave_sync();

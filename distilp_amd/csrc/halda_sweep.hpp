@@ -1723,6 +1723,24 @@ __device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const Kslot
     // part 1 reaches its leaf scan (else it publishes nothing this wave needs: post at once)
     bool pending = live && kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax);
     if (live && lane == 0) ar->alt_best[h] = kInf;
+    // an optimistic part 1 (rows finite at both ends: dp_pass_lanes) leaves phase 0 to this wave: the
+    // unconstrained allocation into the split slot's st0, then the publication part 1's scan awaits
+    if (h == 0 && pending) {
+        const int M = fd.M, R1 = W - M + 1, RS = odd_stride(R1);
+        const bool act = lane < M;
+        const WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
+        const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
+        if (leaf_ends_finite(G, R1, act, sg)) {
+            const int hi = act ? R1 - 1 : -1;
+            int e = 0;
+            phase0_greedy(w.G, RS, R1 - 1, sg, act, hi, e);
+            const double s_inf = sg.sum_f64(act ? G[e] : 0.0);
+            const double hmax = sg.max_f64(act ? fmax(0.0, H[e]) : 0.0);
+            if (act) w.st0[lane] = e;
+            split_publish(ar, lane, act, act ? 0 : R1, hi, s_inf, double(k - 1) * hmax + s_inf, 0,
+                          sg.sum_i(act ? R1 - 1 : 0));
+        }
+    }
     while (__ballot(pending)) {
         const int pb = pending ? __hip_atomic_load(&ar->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
         if (pending && pb != 0) {  // segment-uniform
@@ -1837,7 +1855,7 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
 #ifdef HALDA_STAMPS
-        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split,
+        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false,
                            int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
                                ? g_halda_scanprof + (int64_t(blockIdx.x) * SA.n_slot + q) * kScanProf
                                : nullptr};

@@ -100,7 +100,8 @@ def scan_range(G, H, kc, t_start=None, t_stop=INF):
 
 def split_cuts(G, H, n_parts):
     """ScanSplit's cuts: H at cap(T0) + 2 (and + 3) over the devices with an opening past T0; two parts:
-    the lower median of the first, three: its lower quartile and the lower median of the second."""
+    the value of rank (n - 1) * 5 / 8 of the first (the kernel's), three: its lower quartile and the
+    lower median of the second."""
     M, R1 = G.shape
     fin = np.isfinite(G)
     lo = [int(np.argmax(fin[i])) for i in range(M)]
@@ -115,7 +116,7 @@ def split_cuts(G, H, n_parts):
         return [INF] * (n_parts - 1)
     v2 = sorted(H[i][min(cap[i] + 2, hi[i])] for i in has)
     if n_parts == 2:
-        return [v2[(len(v2) - 1) // 2]]
+        return [v2[(len(v2) - 1) * 5 // 8]]
     v3 = sorted(H[i][min(cap[i] + 3, hi[i])] for i in has)
     a, b = v2[(len(v2) - 1) // 4], v3[(len(v3) - 1) // 2]
     return [min(a, b), max(a, b)]
