@@ -1307,11 +1307,12 @@ __device__ inline void phase0_greedy(const double *Gall, int RS, int need, const
 // start at R1 / -1 / 0 / true / true.
 __device__ inline void leaf_scan(const double *G, const double *H, int R1, bool act, int &lo, int &hi, int &cnt,
                                  bool &ok, bool &mono) {
-    // The row in chunks of 8 entries, the next chunk's 16 LDS reads issued before this chunk is
-    // checked (one LDS latency for the whole row, not one per entry). No chain between entries: each
-    // entry is checked against its two predecessors (g1, g2; d1 = g1 - g2), which in a contiguous
-    // finite range are the sequential scan's prev / dprev, bit for bit; a gap in the range fails the
-    // contiguity test at the end, as the sequential scan's "hi == e - 1" fails at the entry after it.
+    // The row in chunks of 8 entries, the chunk's 16 LDS reads issued together (one LDS latency per
+    // chunk, not one per entry; a prefetch of the next chunk measured no faster and cost the k-slot
+    // kernel 5 VGPRs). No chain between entries: each entry is checked against its two predecessors
+    // (g1, g2; d1 = g1 - g2), which in a contiguous finite range are the sequential scan's prev / dprev,
+    // bit for bit; a gap in the range fails the contiguity test at the end, as the sequential scan's
+    // "hi == e - 1" fails at the entry after it.
     if (act) {
         double gc[8], hc[8];
         auto load = [&](int e0, double (&g)[8], double (&h)[8]) {
@@ -1322,12 +1323,10 @@ __device__ inline void leaf_scan(const double *G, const double *H, int R1, bool 
                 h[t] = H[e];
             }
         };
-        load(0, gc, hc);
         double g1 = kInf, d1 = -kInf, h1 = -kInf;
         bool f1 = false, f2 = false;
         for (int e0 = 0; e0 < R1; e0 += 8) {
-            double gx[8], hx[8];
-            load(e0 + 8, gx, hx);  // the next chunk (clamped: in the row)
+            load(e0, gc, hc);
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 const int e = e0 + t;
@@ -1345,11 +1344,6 @@ __device__ inline void leaf_scan(const double *G, const double *H, int R1, bool 
                 h1 = h;
                 f2 = f1;
                 f1 = fin;
-            }
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                gc[t] = gx[t];
-                hc[t] = hx[t];
             }
         }
         ok = ok && (cnt == 0 || cnt == hi - lo + 1);
