@@ -76,6 +76,7 @@ struct Ctx {
     bool fleet_kslot = false;                    // fused sweep: the first launch was the k-slot kernel
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     int kslot_split = 2;                         // k-slot launch: the longest scan split over 2 waves (0: unsplit)
+    bool kslot_opt = true;                       // ... its part 1 optimistic (leaf checks / phase 0 by other waves)
     int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters; 2.5x
                                                  // measured best of 4..12)
     bool fleet_timed = false;
@@ -461,6 +462,7 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
         }
     }
     SA.crit_w4 = c->kslot_crit_w4;
+    SA.opt = c->kslot_opt ? 1 : 0;
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
     if (SA.helper >= 0) kslot_lds += int64_t(64 / kSegLanes) * int64_t(sizeof(SplitArea));
@@ -967,15 +969,16 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
 int halda_set_fleets_path(void *ctx, int path) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return fail(HALDA_E_ARG, "NULL ctx");
-    if (path < 0 || path > 5)
+    if (path < 0 || path > 6)
         return fail(HALDA_E_ARG, "path must be 0 (CSR), 1 (fused), 2 (fused, one fleet per wave), 3 (fused, k = 1 "
                                  "by DP), 4 (fused, segment kernel instead of the k-slot kernel), 5 (fused, the "
-                                 "k-slot scan unsplit)");
+                                 "k-slot scan unsplit), 6 (fused, the k-slot split scan in sequential order)");
     c->fleets_fused = path != 0;
-    c->seg_sweep = path == 1 || path == 4 || path == 5;
-    c->kslot_sweep = path == 1 || path == 5;
+    c->seg_sweep = path == 1 || path == 4 || path == 5 || path == 6;
+    c->kslot_sweep = path == 1 || path == 5 || path == 6;
     c->k1_force_dp = path == 3;
     c->kslot_split = path == 5 ? 0 : 2;
+    c->kslot_opt = path != 6;
     ++c->path_gen;
     return HALDA_OK;
 }

@@ -1013,6 +1013,7 @@ struct ScanSplit {
     int n_parts = 0;  // 2 (split) or 0
     SplitArea *ar = nullptr;
     bool fetch = false;  // part 1: s_inf / best0 come from the helper's phase 0 (published in ar)
+    bool opt = false;    // part 1 may take rows finite at both ends without checking them (dp_pass_lanes)
 #ifdef HALDA_STAMPS
     unsigned long long *prof = nullptr;  // g_halda_scanprof of this wave (part 1 only)
 #endif
@@ -1376,7 +1377,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
     // part 1 of a split scan whose rows are finite at both ends takes them as [0, R1 - 1] and goes on
     // at once: another wave checks them meanwhile (kslot_check) and the verdict is awaited before this
     // returns (a failed check returns -1, as the check here would have); the helper makes phase 0
-    const bool opt = sp.part == 1 && leaf_ends_finite(G, R1, act, sg);
+    const bool opt = sp.part == 1 && sp.opt && leaf_ends_finite(G, R1, act, sg);
     if (opt) {
         if (act) {
             lo = 0;
@@ -1439,7 +1440,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
 #endif
         LeafInfo lf = li;
         nodes = 1;
-        kc_scan_incremental(w, I, sg, 0.0, 0.0, nodes, lf, ScanSplit{sp.part, sp.n_parts, sp.ar, true
+        kc_scan_incremental(w, I, sg, 0.0, 0.0, nodes, lf, ScanSplit{sp.part, sp.n_parts, sp.ar, true, true
 #ifdef HALDA_STAMPS
                                                                      , sp.prof
 #endif

@@ -1350,6 +1350,7 @@ struct SlotArgs {
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
     int rec_off;               // LDS byte offset of the workgroup's device records (KslotRecs)
     int check_wave;            // the wave that checks the split slot's leaves after its own slot (-1: none)
+    int opt;                   // 1: an optimistic part 1 where its rows allow (0: the sequential order, a test path)
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
 };
 static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
@@ -1695,7 +1696,7 @@ __device__ void kslot_check(const SweepArgs &A, const SlotArgs &SA, const KslotF
                             const Seg<kSegLanes> &sg, unsigned char *smem, int seg, bool live) {
     const int p = SA.helper, lane = sg.sl;
     const int j = SA.j[p], k = A.ks[j], W = A.Ws[j];
-    if (!live || !kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) return;
+    if (!SA.opt || !live || !kslot_uses_tables(fd, k, W, SA.r1[p], SA.tab[p], A.mmax)) return;
     const int M = fd.M, R1 = W - M + 1, RS = odd_stride(R1);
     const bool act = lane < M;
     const WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
@@ -1730,7 +1731,7 @@ __device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const Kslot
         const bool act = lane < M;
         const WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
         const double *G = w.G + int64_t(act ? lane : 0) * RS, *H = w.H + int64_t(act ? lane : 0) * RS;
-        if (leaf_ends_finite(G, R1, act, sg)) {
+        if (SA.opt && leaf_ends_finite(G, R1, act, sg)) {
             const int hi = act ? R1 - 1 : -1;
             int e = 0;
             phase0_greedy(w.G, RS, R1 - 1, sg, act, hi, e);
@@ -1855,12 +1856,12 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
 #ifdef HALDA_STAMPS
-        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false,
+        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0,
                            int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
                                ? g_halda_scanprof + (int64_t(blockIdx.x) * SA.n_slot + q) * kScanProf
                                : nullptr};
 #else
-        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split};
+        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0};
 #endif
         if (f < nf)
             sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);

@@ -286,15 +286,16 @@ class HaldaContext:
             raise RuntimeError(f"halda_last_kernel_ms failed ({rc}): {last_error(self.lib)}")
         return ms.value
 
-    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3, "seg": 4, "kslot_unsplit": 5}
+    FLEET_PATHS = {"csr": 0, "fused": 1, "wave": 2, "dp": 3, "seg": 4, "kslot_unsplit": 5, "kslot_sequential": 6}
 
     def set_fleets_path(self, path) -> None:
         """halda_solve_fleets on the fused sweep ("fused" / True, default: fleets of at most 16 devices
         four per wave, one wave per open k -- the k-slot kernel), the same with the segment kernel
         (four fleets per wave, every k in turn: "seg"), the fused sweep one fleet per wave ("wave"), the CSR
         pipeline ("csr" / False), or (test paths) the fused sweep with every k = 1 solve of its
-        register launch done by the exact DP it falls back to ("dp"), or with the k-slot kernel's
-        k = 2 threshold scan unsplit ("kslot_unsplit"; the default splits it over two waves)."""
+        register launch done by the exact DP it falls back to ("dp"), with the k-slot kernel's
+        k = 2 threshold scan unsplit ("kslot_unsplit"; the default splits it over two waves), or split
+        in sequential order ("kslot_sequential": part 1 makes its leaf checks and phase 0 itself)."""
         code = self.FLEET_PATHS[path] if isinstance(path, str) else int(bool(path))
         rc = self.lib.halda_set_fleets_path(self.ctx, code)
         if rc != 0:

@@ -228,6 +228,9 @@ void halda_fleets_plan_free(void *plan);
  * 4 the fused sweep with the segment kernel instead of the k-slot kernel;
  * 5 (test path) the fused sweep with the k-slot kernel's k = 2 threshold scan unsplit (path 1 splits
  *   it over two waves);
+ * 6 (test path) the fused sweep with the k-slot kernel's split scan in sequential order (path 1 lets
+ *   its part 1 take rows finite at both ends unchecked, the leaf checks and phase 0 made by other waves
+ *   of the workgroup; here part 1 makes them itself, as it does for any other row);
  * 0 the CSR pipeline (lowering kernel -> the halda_solve_batch kernels -> pick kernel), which also
  *   keeps the lowered batch for halda_last_lowered. All give the same statuses, x and k.
  * HALDA_E_ARG for any other path. */

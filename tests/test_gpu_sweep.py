@@ -113,6 +113,10 @@ def test_multi_device_context_equals_single(llama_online_model):
     # the k = 2 threshold scan unsplit (the default splits it in two)
     ("kslot_unsplit", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
     ("kslot_unsplit", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
+    # the split scan in sequential order (part 1 makes its own leaf checks and phase 0; the default
+    # leaves them to other waves of the workgroup for rows finite at both ends)
+    ("kslot_sequential", "halda_sweep_kslot_kernel", [1 + (s * 7) % 16 for s in range(300)]),
+    ("kslot_sequential", "halda_sweep_kslot_kernel", [16] * 200 + [12] * 57),
     ("seg", "halda_sweep_seg_kernel", [1 + (s * 7) % 16 for s in range(300)]),
 ])
 def test_segment_sweep_equals_one_fleet_per_wave(llama_online_model, path, kernel, sizes):

@@ -8,7 +8,8 @@ exact). These fleets make such ties certain: the reference's own "same device tw
 batches of more than 64 fleets, so halda_solve_fleets takes the default k-slot kernel. Per (fleet, k)
 against the exact oracle (status; c.x and the objective within 1e-9; (w, n) where the optimum is
 unique), the best k against the oracle's sweep (ascending k, strict <, halda_p_solver.py:391-412), and
-every other scan layout (unsplit k-slot, segment, one fleet per wave, the CSR pipeline) likewise."""
+every other scan layout (unsplit k-slot, the split in sequential order, segment, one fleet per wave,
+the CSR pipeline) likewise."""
 
 import contextlib
 import io
@@ -40,6 +41,7 @@ def _ks(model):
 PATHS = {  # halda_set_fleets_path name -> the launch that must have run
     "fused": "halda_sweep_kslot_kernel",        # default: k-slot kernel, k = 2 scan split over two waves
     "kslot_unsplit": "halda_sweep_kslot_kernel",
+    "kslot_sequential": "halda_sweep_kslot_kernel",  # the split's part 1 makes its leaf checks / phase 0
     "seg": "halda_sweep_seg_kernel",             # four fleets per wave, every k in turn
     "wave": "halda_sweep_tables_kernel",         # one fleet per wave (64-lane threshold scan)
     "csr": "halda_solve_kernel",                 # lowered CSR -> general kernel (k > 1)
