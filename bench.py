@@ -232,13 +232,19 @@ def run_cpu_baseline(budget_s: float, M: int):
 HOST_ENQUEUE = {}  # per timed leg: host seconds to enqueue its K steps (before the final synchronize)
 
 
-def timed(step, steps, torch, dev, dist, world, tag=None):
+def timed(step, steps, torch, dev, dist, world, tag=None, many=None):
+    """Seconds for `steps` steps between barrier + synchronize on both sides (max over ranks). `many`,
+    when given, enqueues all of them in one call (the k-sweep legs: halda_fleets_plan_launch_many, one
+    kernel launch per step from C, no Python round trip per step); else step() runs `steps` times."""
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    if many is not None:
+        many(steps)
+    else:
+        for _ in range(steps):
+            step()
     if tag:
         HOST_ENQUEUE[tag] = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
@@ -340,13 +346,16 @@ def sweep_bytes(table) -> int:
     return int(sum(DEV_FIELDS * int(m) + 8 + 4 + 8 + 8 * int(m) for m in sizes))
 
 
-def timed_events(step, steps, torch, dev, stream):
+def timed_events(step, steps, torch, dev, stream, many=None):
     """Device time per step of `steps` launches on `stream`, from HIP events recorded on that stream."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     e0.record(stream)
-    for _ in range(steps):
-        step()
+    if many is not None:
+        many(steps)
+    else:
+        for _ in range(steps):
+            step()
     e1.record(stream)
     torch.cuda.synchronize(dev)
     return e0.elapsed_time(e1) / steps
@@ -439,7 +448,7 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     L = 80 (k = 1, 2, 4, 5 feasible: the k > 1 MILPs of halda_p_solver.py:391-412 are solved here), one
     halda_solve_fleets k-sweep per step from resident tables; its own roofline from the one-stream launch
     time of its dominant kernel."""
-    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation, fleet_table
 
     M2 = 16
     table = fleet_table(build_fleets(range(C3_FLEETS), M2), model)
@@ -448,6 +457,15 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     for t in tabs:
         t.plan(ctx)
     turn = [0]
+    rot2, rot1 = PlanRotation(tabs, ctx, srefs), PlanRotation(tabs, ctx, [stream.cuda_stream])
+
+    def many2(k):
+        rot2.launch(turn[0], k)
+        turn[0] += k
+
+    def many1(k):
+        rot1.launch(turn[0], k)
+        turn[0] += k
 
     def step2():
         tabs[turn[0] % n].launch(ctx, srefs[turn[0] % len(srefs)])
@@ -471,8 +489,8 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     if not (bk > 0).all():
         raise RuntimeError("C2: a fleet without a feasible k")
     steps = max(10, args.steps // 4)
-    el2 = timed(step2, steps, torch, dev, None, 1)
-    ev1 = timed_events(step1, steps, torch, dev, stream)
+    el2 = timed(step2, steps, torch, dev, None, 1, many=many2)
+    ev1 = timed_events(step1, steps, torch, dev, stream, many=many1)
     ctx.set_timing(True)
     per = []
     for _ in range(5):
@@ -634,7 +652,7 @@ def main():
 
     from distilp_amd.solver._libhalda import get_context
     from distilp_amd.solver.batch import assemble
-    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation, fleet_table
     from distilp_amd.solver.lower import lower_fleet
 
     t_setup = time.perf_counter()
@@ -666,6 +684,18 @@ def main():
         sweeps[turn[0] % n_sw].launch(ctx, sref)
         turn[0] += 1
 
+    # the timed regions enqueue their steps from C (the same launches, the same rotation over the
+    # resident copies and streams as the step functions above)
+    rot2, rot1 = None, None
+
+    def sweep_many(k):
+        rot2.launch(turn[0], k)
+        turn[0] += k
+
+    def sweep_many_one_stream(k):
+        rot1.launch(turn[0], k)
+        turn[0] += k
+
     # ---- solve-only leg: the same fleets lowered on the host, CSR batch resident in HBM
     lowered = [lower_fleet(devs, model, "4bit") for devs in fleets]
     batch, refs = assemble(lowered, [ks] * len(lowered))
@@ -690,6 +720,7 @@ def main():
     # prepared launches (halda_fleets_plan_create) are set-up, not steps
     for t in sweeps:
         t.plan(ctx)
+    rot2, rot1 = PlanRotation(sweeps, ctx, srefs), PlanRotation(sweeps, ctx, [sref])
     # warm-up and sanity: the sweep's per-fleet answers equal the solve-only leg's k = 1 solves (at least
     # one warm-up step per stream, so that no stream meets its first launch inside a timed region)
     for _ in range(max(args.warmup, len(srefs))):
@@ -705,9 +736,9 @@ def main():
         raise RuntimeError("a fleet without a feasible k in the sweep")
 
     ctx.set_timing(False)  # no per-launch instrumentation events inside the timed regions
-    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world, tag="headline")
-    el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world)
-    sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream)
+    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world, tag="headline", many=sweep_many)
+    el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world, many=sweep_many_one_stream)
+    sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream, many=sweep_many_one_stream)
     el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
     el_solve1 = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
     el_strong = None
@@ -724,9 +755,15 @@ def main():
             s_sweeps[sturn[0] % n_st].launch(ctx, srefs[sturn[0] % len(srefs)])
             sturn[0] += 1
 
+        srot = PlanRotation(s_sweeps, ctx, srefs)
+
+        def strong_many(k):
+            srot.launch(sturn[0], k)
+            sturn[0] += k
+
         for _ in range(max(args.warmup, len(srefs))):
             strong_step()
-        el_strong = timed(strong_step, args.steps, torch, dev, dist, world)
+        el_strong = timed(strong_step, args.steps, torch, dev, dist, world, many=strong_many)
 
     # per-launch device times (HIP events recorded by libhalda on the kernels' stream), after the
     # timed regions; the dominant launch of each leg is the longest

@@ -1249,6 +1249,18 @@ int halda_fleets_plan_launch(void *plan, void *stream) {
     return run_sweep(c, P->p, stream ? static_cast<hipStream_t>(stream) : c->stream);
 }
 
+int halda_fleets_plan_launch_many(void *const *plans, int32_t n_plans, void *const *streams, int32_t n_streams,
+                                  int64_t first, int32_t steps) {
+    if (!plans || !streams || n_plans <= 0 || n_streams <= 0 || steps < 0 || first < 0)
+        return fail(HALDA_E_ARG, "halda_fleets_plan_launch_many: NULL arrays or bad counts");
+    for (int32_t t = 0; t < steps; ++t) {
+        const int64_t i = first + t;
+        const int rc = halda_fleets_plan_launch(plans[i % n_plans], streams[i % n_streams]);
+        if (rc != HALDA_OK) return rc;
+    }
+    return HALDA_OK;
+}
+
 void halda_fleets_plan_free(void *plan) { delete static_cast<FleetsPlan *>(plan); }
 
 // Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.

@@ -107,6 +107,10 @@ def _bind(lib):
     lib.halda_fleets_plan_launch.restype = ctypes.c_int
     lib.halda_fleets_plan_free.argtypes = [ctypes.c_void_p]
     lib.halda_fleets_plan_free.restype = None
+    lib.halda_fleets_plan_launch_many.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
+                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int64,
+                                                  ctypes.c_int32]
+    lib.halda_fleets_plan_launch_many.restype = ctypes.c_int
     lib._fleets_bound = True
     return lib
 
@@ -745,6 +749,28 @@ class RcclComm:
         if getattr(self, "comm", None):
             self.lib.halda_comm_destroy(self.comm)
             self.comm = None
+
+
+class PlanRotation:
+    """Prepared launches of several resident tables on one context, launched in rotation over
+    streams by one C call per group of steps (halda_fleets_plan_launch_many): step i runs table
+    i % len(tables) on stream i % len(streams). A streaming caller's loop without a Python round trip
+    per batch."""
+
+    def __init__(self, tables, ctx, streams):
+        plans = [t.plan(ctx)[1] for t in tables]
+        self.ctx = ctx
+        self.lib = _bind(ctx.lib)
+        self.n_p, self.n_s = len(plans), len(streams)
+        self.plans = (ctypes.c_void_p * self.n_p)(*[p.value for p in plans])
+        self.streams = (ctypes.c_void_p * self.n_s)(*[ctypes.c_void_p(int(x)).value for x in streams])
+        self.tables = tables  # (the plans live with them)
+
+    def launch(self, first: int, steps: int) -> None:
+        with self.ctx._lock:
+            rc = self.lib.halda_fleets_plan_launch_many(self.plans, self.n_p, self.streams, self.n_s, first, steps)
+        if rc != 0:
+            raise RuntimeError(f"halda_fleets_plan_launch_many failed ({rc}): {last_error(self.lib)}")
 
 
 def launch_sharded_emulated(dt: "DeviceFleetTable", ctx, world: int, report_rank: int, stream: int) -> None:

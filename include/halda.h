@@ -215,6 +215,11 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
 int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                              int32_t n_k, const halda_fleet_result *out, void **plan);
 int halda_fleets_plan_launch(void *plan, void *stream);
+/* `steps` launches in one call, launch t of plans[(first + t) % n_plans] on streams[(first + t) %
+ * n_streams] (a streaming caller's batches rotating over resident tables and streams, without a host
+ * round trip per batch); stops at the first failing launch and returns its code. */
+int halda_fleets_plan_launch_many(void *const *plans, int32_t n_plans, void *const *streams, int32_t n_streams,
+                                  int64_t first, int32_t steps);
 void halda_fleets_plan_free(void *plan);
 
 /* How halda_solve_fleets runs (default 1; HALDA_FLEETS_PATH=csr / =wave at halda_init select 0 / 2):
