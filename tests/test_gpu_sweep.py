@@ -353,6 +353,41 @@ def test_prepared_plan_equals_solve_fleets(llama_online_model, sizes):
     dt.replan()
 
 
+def test_plan_launch_many_rotates_tables_and_streams(llama_online_model):
+    """halda_fleets_plan_launch_many (the bench's timed k-sweep steps): step i runs table i % T on
+    stream i % S; three differently seeded C2-shaped tables over two streams, 7 steps from an odd first
+    index, give each table the results of its own synchronous halda_solve_fleets, bit for bit."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation
+
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    tabs, wants = [], []
+    for t in range(3):
+        fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(26000 + 100 * t + s, 16)] for s in range(80)]
+        table = fleet_table(fleets, llama_online_model)
+        wants.append(solve_table(table, llama_online_model, ks, 0.5))
+        tabs.append(DeviceFleetTable(table, llama_online_model, ks, 0.5, dev, want_per_k=True))
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    rot = PlanRotation(tabs, ctx, [s.cuda_stream for s in streams])
+    for t in tabs:
+        for f in ("best_k", "obj_value", "w", "n", "status", "obj_by_k"):
+            t.out[f].zero_()
+    torch.cuda.synchronize(dev)
+    rot.launch(5, 7)
+    torch.cuda.synchronize(dev)
+    for t, want in zip(tabs, wants):
+        assert np.array_equal(t.out["best_k"].cpu().numpy(), want.best_k)
+        assert np.array_equal(t.out["obj_value"].cpu().numpy(), want.obj_value)
+        assert np.array_equal(t.out["w"].cpu().numpy(), want.w) and np.array_equal(t.out["n"].cpu().numpy(), want.n)
+        assert np.array_equal(t.out["status"].cpu().numpy(), want.status.ravel())
+        assert np.array_equal(t.out["obj_by_k"].cpu().numpy(), want.obj_by_k.ravel())
+    with pytest.raises(RuntimeError):
+        PlanRotation(tabs, ctx, []).launch(0, 1)
+
+
 def test_prepared_plan_follows_the_context_path(llama_online_model):
     """A prepared plan re-plans when the context's path changes (halda_set_fleets_path): C2-shaped batch,
     planned on the k-slot path, then launched on the one-fleet-per-wave and CSR paths -- each runs its
