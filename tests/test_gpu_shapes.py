@@ -134,3 +134,39 @@ def test_big_table_launches_on_two_streams(llama_online_model):
         assert np.array_equal(d.out["obj_value"].cpu().numpy(), w.obj_value)
         assert np.array_equal(d.out["status"].cpu().numpy(), w.status.ravel())
         assert np.array_equal(d.out["obj_by_k"].cpu().numpy(), w.obj_by_k.ravel())
+
+
+@pytest.mark.parametrize("L,M", [(96, 12), (96, 16), (120, 16), (48, 8)])
+def test_kslot_kernel_other_L(llama_online_model, L, M):
+    """The k-slot kernel (more than 64 fleets of at most 16 devices, one wave per open k) on other layer
+    counts than C2's L = 80: other open k's, another split slot / helper / leaf-check wave (the split
+    slot is the largest table, the checker the smallest other one), default path and the split in
+    sequential order against the one-fleet-per-wave sweep bit for bit, and 4 fleets' sweeps against the
+    exact oracle."""
+    from distilp_amd.solver.fleets import fleet_table, solve_table
+
+    model = llama_online_model.model_copy(update={"L": L})
+    ks = _factors(L)
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(31000 + s, M)] for s in range(72)]
+    table = fleet_table(fleets, model)
+    ctx = get_context(0)
+    runs = {}
+    try:
+        ctx.set_timing(True)
+        for path in ("fused", "kslot_sequential", "wave"):
+            ctx.set_fleets_path(path)
+            runs[path] = solve_table(table, model, ks, 0.5, want_x=True)
+            if path != "wave":
+                assert "halda_sweep_kslot_kernel" in ctx.last_fleet_ms(), (path, ctx.last_fleet_ms())
+    finally:
+        ctx.set_fleets_path("fused")
+        ctx.set_timing(False)
+    for path in ("fused", "kslot_sequential"):
+        for f in ("status", "obj_by_k", "best_k", "obj_value", "w", "n"):
+            assert np.array_equal(getattr(runs[path], f), getattr(runs["wave"], f)), (path, f)
+        N = 7 * M + 1
+        assert np.array_equal(runs[path].x[:, :, :N], runs["wave"].x[:, :, :N]), path
+    res = runs["fused"]
+    for fi in range(4):
+        want, _ = mo.halda_solve_oracle(fleets[fi], model, k_candidates=ks, kv_bits="4bit", solver="exact")
+        assert res.best_k[fi] == want["k"] and _close(float(res.obj_value[fi]), want["obj_value"]), (fi, want)
