@@ -77,8 +77,9 @@ struct Ctx {
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     int kslot_split = 2;                         // k-slot launch: the longest scan split over 2 waves (0: unsplit)
     bool kslot_opt = true;                       // ... its part 1 optimistic (leaf checks / phase 0 by other waves)
-    int kslot_crit_w4 = 10;                      // k-slot table share of the critical slot's wave (quarters; 2.5x
-                                                 // measured best of 4..12)
+    int kslot_crit_w4 = 8;                       // k-slot table share of the critical slot's wave (quarters; 2x:
+                                                 // measured best of 7..12 since part 1 leaves its leaf checks and
+                                                 // phase 0 to other waves; 2.5x before)
     bool fleet_timed = false;
     bool fleets_fused = true;      // halda_solve_fleets: the fused sweep (default) or the CSR pipeline
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
