@@ -16,7 +16,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--pin", action="store_true", help="pin this process to one core, GC off")
+    ap.add_argument("--spin-flags", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) first")
+    ap.add_argument("--hot-us", type=float, default=0.0, help="busy-wait this long on the host before each region")
     args = ap.parse_args()
+    if args.spin_flags:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        print("hipSetDeviceFlags(spin):", hip.hipSetDeviceFlags(1))
     if args.pin:
         import gc
         import os
@@ -49,6 +55,10 @@ def main():
     torch.cuda.synchronize(dev)
     for r in range(args.rounds):
         torch.cuda.synchronize(dev)
+        if args.hot_us:
+            th = time.perf_counter_ns() + int(args.hot_us * 1e3)
+            while time.perf_counter_ns() < th:
+                pass
         ts = []
         t0 = time.perf_counter_ns()
         for _ in range(args.steps):
