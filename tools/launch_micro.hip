@@ -27,6 +27,8 @@ int main() {
     hipFunction_t fn;
     if (hipGetFuncBySymbol(&fn, reinterpret_cast<const void *>(k_big)) != hipSuccess) printf("hipGetFuncBySymbol failed\n");
     const int N = 2000;
+    for (int G : {1, 1024}) {
+    printf("grid %d x 64\n", G);
     for (int rep = 0; rep < 3; ++rep) {
         for (int mode = 0; mode < 3; ++mode) {
             hipDeviceSynchronize();
@@ -34,10 +36,10 @@ int main() {
             for (int i = 0; i < N; ++i) {
                 hipStream_t s = (i & 1) ? s2 : s1;
                 if (mode == 0) {
-                    hipLaunchKernelGGL(k_big, dim3(1024), dim3(256), 0, s, a, out);
+                    hipLaunchKernelGGL(k_big, dim3(G), dim3(64), 0, s, a, out);
                 } else if (mode == 1) {
                     void *args[] = {&a, &out};
-                    hipModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+                    hipModuleLaunchKernel(fn, G, 1, 1, 64, 1, 1, 0, s, args, nullptr);
                 } else {
                     struct {
                         Big a;
@@ -45,7 +47,7 @@ int main() {
                     } pk{a, out};
                     size_t sz = sizeof(pk);
                     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &pk, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-                    hipModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+                    hipModuleLaunchKernel(fn, G, 1, 1, 64, 1, 1, 0, s, nullptr, cfg);
                 }
             }
             auto t1 = std::chrono::steady_clock::now();
@@ -56,6 +58,7 @@ int main() {
                    std::chrono::duration<double, std::micro>(t1 - t0).count() / N,
                    std::chrono::duration<double, std::micro>(t2 - t0).count() / N);
         }
+    }
     }
     return 0;
 }
