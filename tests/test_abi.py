@@ -79,3 +79,28 @@ def test_integration_md_stub_is_the_committed_file():
     md = (REPO / "INTEGRATION.md").read_text()
     code = (REPO / "integration" / "halda_milp.py").read_text()
     assert "```python\n" + code + "```" in md
+
+
+def test_plan_entry_points_reject_bad_arguments(lib):
+    """The plan / path entry points validate their arguments before any HIP call (HALDA_E_ARG = -22,
+    include/halda.h:56), so a binding's mistakes fail loudly on any host."""
+    raw = ctypes.CDLL(str(lh.LIB_PATH))
+    P = ctypes.c_void_p
+    many = raw.halda_fleets_plan_launch_many
+    many.argtypes = [ctypes.POINTER(P), ctypes.c_int32, ctypes.POINTER(P), ctypes.c_int32, ctypes.c_int64,
+                     ctypes.c_int32]
+    many.restype = ctypes.c_int
+    plans, streams = (P * 1)(None), (P * 1)(None)
+    assert many(None, 1, streams, 1, 0, 1) == -22
+    assert "launch_many" in lh.last_error(lib)
+    assert many(plans, 0, streams, 1, 0, 1) == -22
+    assert many(plans, 1, streams, 0, 0, 1) == -22
+    assert many(plans, 1, streams, 1, -1, 1) == -22
+    assert many(plans, 1, streams, 1, 0, -1) == -22
+    assert many(plans, 1, streams, 1, 0, 0) == 0  # no steps: nothing launched
+    assert many(plans, 1, streams, 1, 0, 1) == -22  # the NULL plan, from halda_fleets_plan_launch
+    assert "NULL plan" in lh.last_error(lib)
+    raw.halda_fleets_plan_launch.argtypes = [P, P]
+    assert raw.halda_fleets_plan_launch(None, None) == -22
+    raw.halda_set_fleets_path.argtypes = [P, ctypes.c_int]
+    assert raw.halda_set_fleets_path(None, 1) == -22
