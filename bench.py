@@ -333,6 +333,36 @@ def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None, workload="c3")
             "launch_ms": phase_ms}
 
 
+def group_roofline(launch_ms, steps, batch_bytes, n_fleets, single):
+    """Roofline of the headline's launch as launched: ONE halda_sweep_steps_kernel launch of `steps`
+    batches, algorithmic bytes = steps x one batch's, time = HIP events around that launch
+    on its stream; HBM traffic and the VALU count from this build's rocprofv3 profiles (per launch of
+    the same K). `single` (the per-batch kernel's own roofline, one launch per batch) is kept beside it."""
+    alg = steps * batch_bytes
+    achieved = alg / (launch_ms * 1e-3) / 1e9
+    kern = "halda_sweep_steps_kernel"
+    vp = valu_profile(kern, "c3_steps")
+    if vp and vp.get("items"):
+        # VALU per (fleet, batch) item of the profiled launch, times this launch's items
+        need = vp["valu_per_wave"] * vp["waves"] / vp["items"] * (steps * n_fleets) * VALU_CYCLES / (
+            N_SIMDS * CLOCK_GHZ * 1e9)
+        valu = {"frac": need / (launch_ms * 1e-3), "valu_per_item": vp["valu_per_wave"] * vp["waves"] / vp["items"],
+                "cycles_per_valu": VALU_CYCLES, "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": vp["source"],
+                "wait_any_frac": vp.get("wait_any_frac")}
+    else:
+        valu = {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
+    traffic = pmc_traffic(kern)
+    if traffic is not None:
+        traffic = traffic.get(str(steps)) if isinstance(traffic, dict) else None
+    roofs = {"hbm": achieved / HBM_PEAK_GBS, "valu_issue": valu["frac"]}
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic, "kernel": kern, "kernel_ms": launch_ms,
+            "kernel_ms_from": "HIP events around one launch of K batches on its stream (median of 3)",
+            "steps_per_launch": steps, "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_per_batch": batch_bytes,
+            "roofs": roofs, "nearest_roof": max((k for k, v in roofs.items() if v is not None), key=lambda k: roofs[k]),
+            "valu_issue": valu, "single_batch_kernel": single}
+
+
 def single_launch_steps(phase_ms):
     dom = max(phase_ms, key=phase_ms.get)
     return all(v < 1e-3 for k, v in phase_ms.items() if k != dom)
@@ -453,7 +483,10 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     M2 = 16
     table = fleet_table(build_fleets(range(C3_FLEETS), M2), model)
     n = max(2, min(32, math.ceil(2 * MALL_BYTES / max(DeviceFleetTable(table, model, KS_L80, 0.5, dev).nbytes(), 1))))
-    tabs = [DeviceFleetTable(table, model, KS_L80, 0.5, dev, want_per_k=True) for _ in range(n)]
+    # the timed steps return what a halda_solve returns per fleet (best k, obj_value, w, n), as the C3
+    # headline does; the per-k statuses are read once from a probe copy
+    tabs = [DeviceFleetTable(table, model, KS_L80, 0.5, dev) for _ in range(n)]
+    probe = DeviceFleetTable(table, model, KS_L80, 0.5, dev, want_per_k=True)
     for t in tabs:
         t.plan(ctx)
     turn = [0]
@@ -482,9 +515,12 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
         step1()
     for _ in range(2 * len(srefs)):
         step2()
+    probe.launch(ctx, stream.cuda_stream)
     torch.cuda.synchronize(dev)
-    st = tabs[(turn[0] - 1) % n].out["status"].cpu().numpy()
+    st = probe.out["status"].cpu().numpy()
     n_opt = int((st == 0).sum())
+    if not np.array_equal(probe.out["best_k"].cpu().numpy(), tabs[0].out["best_k"].cpu().numpy()):
+        raise RuntimeError("C2: the probe copy disagrees with the timed copies")
     bk = tabs[(turn[0] - 1) % n].out["best_k"].cpu().numpy()
     if not (bk > 0).all():
         raise RuntimeError("C2: a fleet without a feasible k")
@@ -652,7 +688,7 @@ def main():
 
     from distilp_amd.solver._libhalda import get_context
     from distilp_amd.solver.batch import assemble
-    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation, fleet_table
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup, PlanRotation, fleet_table
     from distilp_amd.solver.lower import lower_fleet
 
     t_setup = time.perf_counter()
@@ -686,7 +722,13 @@ def main():
 
     # the timed regions enqueue their steps from C (the same launches, the same rotation over the
     # resident copies and streams as the step functions above)
-    rot2, rot1 = None, None
+    rot2, rot1, group = None, None, None
+
+    def sweep_group(k):
+        # the headline: K batches (copy (turn + t) % n_sw each) in ONE launch on one stream
+        # (halda_fleets_group_launch: resident waves prefetch each next (fleet, batch)'s fields)
+        group.launch(turn[0], k, sref)
+        turn[0] += k
 
     def sweep_many(k):
         rot2.launch(turn[0], k)
@@ -721,6 +763,7 @@ def main():
     for t in sweeps:
         t.plan(ctx)
     rot2, rot1 = PlanRotation(sweeps, ctx, srefs), PlanRotation(sweeps, ctx, [sref])
+    group = PlanGroup(sweeps, ctx)
     # warm-up and sanity: the sweep's per-fleet answers equal the solve-only leg's k = 1 solves (at least
     # one warm-up step per stream, so that no stream meets its first launch inside a timed region)
     for _ in range(max(args.warmup, len(srefs))):
@@ -734,11 +777,26 @@ def main():
     bk = sweeps[0].out["best_k"].cpu().numpy()
     if not (bk > 0).all():
         raise RuntimeError("a fleet without a feasible k in the sweep")
+    # the group launch leaves every copy's results bit-identical to its own per-batch launch (checked on
+    # the first copy; every group launch in this process has K steps, so a kernel trace averages alike)
+    ref = {k: v.cpu().numpy().copy() for k, v in sweeps[0].out.items()}
+    for v in sweeps[0].out.values():
+        v.zero_()
+    turn[0] = 0
+    sweep_group(args.steps)
+    torch.cuda.synchronize(dev)
+    for k, v in sweeps[0].out.items():
+        if not np.array_equal(v.cpu().numpy(), ref[k]):
+            raise RuntimeError(f"group launch: {k} differs from the per-batch launch")
 
     ctx.set_timing(False)  # no per-launch instrumentation events inside the timed regions
-    el_sweep = timed(sweep_step, args.steps, torch, dev, dist, world, tag="headline", many=sweep_many)
+    el_sweep = timed(None, args.steps, torch, dev, dist, world, tag="headline", many=sweep_group)
+    el_sweep2 = timed(sweep_step, args.steps, torch, dev, dist, world, tag="per_launch", many=sweep_many)
     el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world, many=sweep_many_one_stream)
     sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream, many=sweep_many_one_stream)
+    # the group launch's own device time (HIP events on its stream around the one launch of K batches)
+    group_ms = statistics.median(timed_events(None, 1, torch, dev, stream, many=lambda _: sweep_group(args.steps))
+                                 for _ in range(3))
     el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
     el_solve1 = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
     el_strong = None
@@ -817,14 +875,26 @@ def main():
                 "rccl_world_size": rccl_world,
                 "resident_copies": n_sw,
             },
-            "one_stream": {"what": "the same k-sweep steps all on one stream (each batch waits for the previous)",
+            "launch": {"what": "the K steps as ONE group launch (halda_fleets_group_launch -> "
+                               "halda_sweep_steps_kernel): batch t reads resident copy (first + t) % copies and writes "
+                               "its results, bit-identical to its own launch; resident waves load each next (fleet, "
+                               "batch)'s fields while solving the current one",
+                       "persistent": group.persistent, "launches_per_region": 1 if group.persistent else args.steps,
+                       "stream": 1},
+            "per_launch": {"what": "the same K steps as K launches (one per batch, halda_fleets_plan_launch_many) "
+                                   "alternating over the streams: two batches in flight",
+                           "ms_per_step": el_sweep2 / args.steps * 1e3, "instances_per_s": total / el_sweep2,
+                           "host_enqueue_ms_per_step": HOST_ENQUEUE["per_launch"] / args.steps * 1e3,
+                           "streams": args.streams},
+            "one_stream": {"what": "the same K steps as K launches all on one stream (each batch waits for the "
+                                   "previous)",
                            "ms_per_step": el_sweep1 / args.steps * 1e3, "instances_per_s": total / el_sweep1},
             "host_enqueue_ms_per_step": HOST_ENQUEUE["headline"] / args.steps * 1e3,
-            "streams": args.streams,
             "feasible_instances_per_s": value * n_opt / batch.n_inst,
             "fleets_per_s": n_fleets_total / el_sweep,
             "time_to_optimal_ms": tto,
-            "roofline": roofline(fl_mean, alg, pmc_traffic, sweep_ev_ms),
+            "roofline": group_roofline(group_ms, args.steps, alg["halda_sweep_kernel"], len(fleets),
+                                       roofline(fl_mean, alg, pmc_traffic, sweep_ev_ms)),
             "solve_only": {
                 "what": "same fleets lowered on the host beforehand; halda_solve_batch_device on the CSR batch "
                         "resident in HBM (the milp() replacement alone); consecutive batches alternate over the "
@@ -847,16 +917,6 @@ def main():
             "cpu_baseline": cpu_base,
             "setup_s": setup_s,
         }
-        rf = line["roofline"]
-        if rf["algorithmic_bytes_per_launch"] and single_launch_steps(fl_mean):
-            # two independent batches in flight on two streams: the step is shorter than one launch, so
-            # this is throughput over overlapped launches, never a kernel fraction
-            a = rf["algorithmic_bytes_per_launch"] / (line["ms_per_step"] * 1e-3) / 1e9
-            line["throughput_overlap"] = {
-                "what": "the headline steps: consecutive batches alternate over two streams, so one batch's field "
-                        "loads overlap the previous batch's compute; algorithmic bytes of one launch over that "
-                        "step time (not a kernel roofline: the kernel itself takes roofline.kernel_ms)",
-                "ms_per_step": line["ms_per_step"], "kernel_ms": rf["kernel_ms"], "alg_GBps_over_step": a}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -49,6 +49,13 @@ int fail(int code, const std::string &msg) {
         if (e_ != hipSuccess) return fail(HALDA_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+struct Ctx;
+// A prepared plan or group bound to a context: halda_free detaches every live one (c = nullptr), so a
+// launch through it after the context is gone fails with HALDA_E_ARG instead of touching freed memory.
+struct CtxHandle {
+    Ctx *c = nullptr;
+};
+
 struct Ctx {
     int device = 0;
     int cus = 256;
@@ -123,14 +130,35 @@ struct Ctx {
         int per_cu;
     } occ[8] = {};
     int n_occ = 0;
+    // The dynamic-LDS limit is a per-function attribute of the whole process: it only ever rises here
+    // (the largest size any plan of any context asked for), so a plan made for a large slice stays
+    // launchable after a smaller one was planned for the same kernel.
+    struct LdsAttr {
+        const void *fn;
+        int64_t lds;
+    };
+    static inline LdsAttr lds_attr[16] = {};
+    static inline int n_lds_attr = 0;
+    static hipError_t ensure_lds(const void *fn, int64_t lds) {
+        int i = 0;
+        while (i < n_lds_attr && lds_attr[i].fn != fn) ++i;
+        if (i < n_lds_attr && lds_attr[i].lds >= lds) return hipSuccess;
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        if (i == n_lds_attr && n_lds_attr < 16) ++n_lds_attr;
+        if (i < 16) lds_attr[i] = LdsAttr{fn, lds};
+        return hipSuccess;
+    }
+    std::vector<CtxHandle *> handles;  // live plans / groups made on this context
+    void detach(CtxHandle *h) { handles.erase(std::remove(handles.begin(), handles.end(), h), handles.end()); }
     hipError_t occupancy(const void *fn, int64_t lds, int *per_cu) {
+        hipError_t e = ensure_lds(fn, lds);
+        if (e != hipSuccess) return e;
         for (int i = 0; i < n_occ; ++i)
             if (occ[i].fn == fn && occ[i].lds == lds) {
                 if (per_cu) *per_cu = occ[i].per_cu;
                 return hipSuccess;
             }
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        if (e != hipSuccess) return e;
         int p = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, fn, 64, size_t(lds));
         if (e != hipSuccess) return e;
@@ -576,6 +604,7 @@ int run_sweep(Ctx *c, SweepPlan &p, hipStream_t s) {
     A.want = 0;
     c->fleet_timed = false;
     c->have_lowered = false;
+    if (p.lds > 0) HIP_TRY(Ctx::ensure_lds(p.fn1, p.lds));
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
     switch (p.kind) {
         case kKslotGated:
@@ -612,6 +641,7 @@ int run_sweep(Ctx *c, SweepPlan &p, hipStream_t s) {
             A.gtab = static_cast<unsigned char *>(c->gtab);
             hipLaunchKernelGGL(halda_sweep_big_kernel, dim3(p.grid2), dim3(64), 0, s, A);
         } else {
+            HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_tables_kernel), p.slice));
             hipLaunchKernelGGL(halda_sweep_tables_kernel, dim3(p.grid2), dim3(64), size_t(p.slice), s, A);
         }
         HIP_TRY(hipGetLastError());
@@ -886,6 +916,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
 void halda_free(void *ctx) {
     Ctx *c = static_cast<Ctx *>(ctx);
     if (!c) return;
+    for (CtxHandle *h : c->handles) h->c = nullptr;  // plans / groups outliving the context fail cleanly
+    c->handles.clear();
     (void)hipSetDevice(c->device);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -1062,8 +1094,7 @@ int check_fleets_args(const halda_model *model, const halda_fleets *fleets, cons
 
 // A prepared k-sweep (halda_fleets_plan_create): the fused sweep's plan, or, when the context runs
 // halda_solve_fleets another way (the CSR pipeline, more than 64 k), the call's arguments.
-struct FleetsPlan {
-    Ctx *c = nullptr;
+struct FleetsPlan : CtxHandle {
     int gen = 0;  // the context's path_gen when planned
     bool fused = false;
     SweepPlan p;
@@ -1230,6 +1261,7 @@ int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fl
         delete P;
         return rc;
     }
+    c->handles.push_back(P);
     *plan = P;
     return HALDA_OK;
 }
@@ -1237,6 +1269,7 @@ int halda_fleets_plan_create(void *ctx, const halda_model *model, const halda_fl
 int halda_fleets_plan_launch(void *plan, void *stream) {
     FleetsPlan *P = static_cast<FleetsPlan *>(plan);
     if (!P) return fail(HALDA_E_ARG, "NULL plan");
+    if (!P->c) return fail(HALDA_E_ARG, "halda_fleets_plan_launch: the plan's context was freed");
     if (P->F.n_fleets <= 0) return HALDA_OK;
     Ctx *c = P->c;
     int cur = -1;
@@ -1262,7 +1295,156 @@ int halda_fleets_plan_launch_many(void *const *plans, int32_t n_plans, void *con
     return HALDA_OK;
 }
 
-void halda_fleets_plan_free(void *plan) { delete static_cast<FleetsPlan *>(plan); }
+void halda_fleets_plan_free(void *plan) {
+    FleetsPlan *P = static_cast<FleetsPlan *>(plan);
+    if (!P) return;
+    if (P->c) P->c->detach(P);
+    delete P;
+}
+
+}  // extern "C"
+
+// ---- groups: `steps` batches over resident tables in one launch (halda_sweep_steps_kernel)
+namespace {
+struct FleetsGroup : CtxHandle {
+    std::vector<FleetsPlan> plans;  // copies: the group does not depend on the caller's plan handles
+    bool persistent = false;        // every plan a register sweep of one shape: the steps kernel applies
+    int gen = 0;                    // the context's path_gen when the group was checked
+    SweepArgs A;                    // the first plan's arguments (shape, model, k list)
+    StepsDesc *desc = nullptr;      // device copy of the plans' tables / results
+    unsigned grid = 0;
+};
+
+bool same_model(const halda_model &a, const halda_model &b) { return std::memcmp(&a, &b, sizeof a) == 0; }
+
+// Whether the group's plans can run as one steps launch, and its descriptors if so.
+int group_check(FleetsGroup *G) {
+    Ctx *c = G->c;
+    G->gen = c->path_gen;
+    G->persistent = false;
+    for (FleetsPlan &P : G->plans) {
+        if (P.gen != c->path_gen) {
+            const int rc = replan(&P);
+            if (rc != HALDA_OK) return rc;
+        }
+    }
+    const FleetsPlan &P0 = G->plans[0];
+    bool ok = P0.fused && P0.p.kind == kRegAlone && P0.p.A.uM > 0 && P0.p.A.uM <= kK1MaxM &&
+              !(P0.p.A.outs & kOutXC) && !P0.p.A.x_off && !P0.p.A.k1dp;
+    for (const FleetsPlan &P : G->plans) {
+        ok = ok && P.fused && P.p.kind == kRegAlone && P.F.n_fleets == P0.F.n_fleets && P.p.A.uM == P0.p.A.uM &&
+             P.p.A.outs == P0.p.A.outs && P.ks == P0.ks && same_model(P.model, P0.model) && !P.p.A.x_off;
+    }
+    if (!ok) return HALDA_OK;
+    std::vector<StepsDesc> h(G->plans.size());
+    for (size_t i = 0; i < h.size(); ++i) {
+        const FleetsPlan &P = G->plans[i];
+        h[i].F = P.F;
+        h[i].out = FleetOut(P.out);
+        int64_t base = 0;  // dev_off[0] of the table (device memory, read once here)
+        HIP_TRY(hipMemcpy(&base, P.F.dev_off, sizeof base, hipMemcpyDeviceToHost));
+        h[i].base = base;
+    }
+    if (!G->desc) HIP_TRY(hipMalloc(&G->desc, sizeof(StepsDesc) * h.size()));
+    HIP_TRY(hipMemcpy(G->desc, h.data(), sizeof(StepsDesc) * h.size(), hipMemcpyHostToDevice));
+    G->A = P0.p.A;
+    // every wave resident at once: the occupancy of the steps kernel (4 waves per SIMD) on every CU,
+    // at most one wave per fleet
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(halda_sweep_steps_kernel),
+                                                         64 * kSweepWavesPerBlock, 0));
+    const int64_t waves = int64_t(std::max(per_cu, 1)) * c->cus * kSweepWavesPerBlock;
+    const int64_t need = (int64_t(P0.F.n_fleets) + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock;
+    G->grid = unsigned(std::max<int64_t>(1, std::min(waves / kSweepWavesPerBlock, need)));
+    G->persistent = true;
+    return HALDA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int halda_fleets_group_create(void *const *plans, int32_t n_plans, void **group, int32_t *persistent) {
+    if (!plans || n_plans <= 0 || !group) return fail(HALDA_E_ARG, "halda_fleets_group_create: NULL arrays or n_plans <= 0");
+    Ctx *c = nullptr;
+    for (int32_t i = 0; i < n_plans; ++i) {
+        const FleetsPlan *P = static_cast<const FleetsPlan *>(plans[i]);
+        if (!P || !P->c) return fail(HALDA_E_ARG, "halda_fleets_group_create: NULL plan or freed context");
+        if (c && P->c != c) return fail(HALDA_E_ARG, "halda_fleets_group_create: plans of different contexts");
+        c = P->c;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    FleetsGroup *G = new FleetsGroup();
+    G->c = c;
+    for (int32_t i = 0; i < n_plans; ++i) G->plans.push_back(*static_cast<const FleetsPlan *>(plans[i]));
+    for (FleetsPlan &P : G->plans) P.c = c;
+    const int rc = group_check(G);
+    if (rc != HALDA_OK) {
+        if (G->desc) (void)hipFree(G->desc);
+        delete G;
+        return rc;
+    }
+    c->handles.push_back(G);
+    *group = G;
+    if (persistent) *persistent = G->persistent ? 1 : 0;
+    return HALDA_OK;
+}
+
+int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *stream) {
+    FleetsGroup *G = static_cast<FleetsGroup *>(group);
+    if (!G) return fail(HALDA_E_ARG, "NULL group");
+    if (!G->c) return fail(HALDA_E_ARG, "halda_fleets_group_launch: the group's context was freed");
+    if (steps < 0 || first < 0) return fail(HALDA_E_ARG, "halda_fleets_group_launch: steps and first must be >= 0");
+    Ctx *c = G->c;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c->device) HIP_TRY(hipSetDevice(c->device));
+    if (G->gen != c->path_gen) {
+        const int rc = group_check(G);
+        if (rc != HALDA_OK) return rc;
+    }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    const int64_t n = int64_t(G->plans.size());
+    if (steps == 0 || G->plans[0].F.n_fleets <= 0) return HALDA_OK;
+    if (!G->persistent) {  // batch by batch, each its own launch(es), in order on the one stream
+        for (int32_t t = 0; t < steps; ++t) {
+            FleetsPlan &P = G->plans[size_t((first + t) % n)];
+            const int rc = P.fused ? run_sweep(c, P.p, s)
+                                   : halda_solve_fleets(c, &P.model, &P.F, P.ks.data(), int32_t(P.ks.size()), &P.out, s);
+            if (rc != HALDA_OK) return rc;
+        }
+        return HALDA_OK;
+    }
+    StepsArgs SG;
+    SG.desc = G->desc;
+    SG.n_desc = int(n);
+    SG.first = int(first % n);
+    SG.steps = steps;
+    c->fleet_timed = false;
+    c->have_lowered = false;
+    if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
+    hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(G->grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
+    HIP_TRY(hipGetLastError());
+    if (c->timing) {
+        HIP_TRY(hipEventRecord(c->evf1, s));
+        c->fleet_timed = true;
+    }
+    c->fleet_two = false;
+    c->fleet_reg_alone = true;
+    c->fleet_seg = false;
+    c->fleet_kslot = false;
+    c->last_fleet_fused = true;
+    return HALDA_OK;
+}
+
+void halda_fleets_group_free(void *group) {
+    FleetsGroup *G = static_cast<FleetsGroup *>(group);
+    if (!G) return;
+    if (G->c) {
+        (void)hipSetDevice(G->c->device);
+        G->c->detach(G);
+    }
+    if (G->desc) (void)hipFree(G->desc);
+    delete G;
+}
 
 // Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.
 constexpr size_t kZeroCopyBytes = size_t(1) << 20;
@@ -1572,6 +1754,10 @@ int halda_solve_fleets_sharded_emulated(void *ctx, int32_t world, int32_t report
         return fail(HALDA_E_ARG, "halda_solve_fleets_sharded_emulated: need 1 <= world <= 16, 0 <= report_rank < world");
     if (!out->best_k || !out->obj_value || !out->w || !out->n) return fail(HALDA_E_ARG, "halda_fleet_result: NULL");
     if (out->x || out->c) return fail(HALDA_E_ARG, "halda_solve_fleets_sharded: x / c are not gathered (pass NULL)");
+    if (fleets->n_fleets > 0) {  // n_k, ks and the arrays before any size is computed or HIP call made
+        const int rc = check_fleets_args(model, fleets, ks, n_k, out);
+        if (rc != HALDA_OK) return rc;
+    }
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     const int64_t nf = fleets->n_fleets;

@@ -738,7 +738,11 @@ __device__ inline void fleet_offsets_regs(const SweepModel &Mo, const DevFields 
     const int hf = sg.bcast(mf.flags, hi);
     const double scpu = sg.bcast(mf.scpu, hi), Tc = sg.bcast(mf.Tc, hi), sdisk = sg.bcast(mf.sdisk, hi);
     const int j = sg.sl & 3;
-    const double num = j == 0 ? Mo.f_out_b1 : j == 1 ? Mo.bvo : j == 2 ? Mo.b_in : Mo.b_out;
+    // the four numerators as register values: a select chain over kernel arguments is otherwise turned
+    // into a per-lane vector load from the argument segment (a vector memory wait of its own)
+    double n0 = Mo.f_out_b1, n1 = Mo.bvo, n2 = Mo.b_in, n3 = Mo.b_out;
+    asm volatile("" : "+s"(n0), "+s"(n1), "+s"(n2), "+s"(n3));
+    const double num = j == 0 ? n0 : j == 1 ? n1 : j == 2 ? n2 : n3;
     const double den = j == 0 ? scpu : j == 1 ? Tc : j == 2 ? Mo.V * sdisk : sdisk;
     const double q = num / den;
     const double q0 = sg.bcast(q, 0), q1 = sg.bcast(q, 1), q2 = sg.bcast(q, 2), q3 = sg.bcast(q, 3);
@@ -834,20 +838,20 @@ __device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
 
 // x / c of one (fleet, k) solution (col layout [w|n|s1|s2|s3|t|z|C] with the fleet's M), written
 // by the lane of each device when the caller asked for them.
-__device__ inline void put_xc(const SweepArgs &A, int64_t inst, int M, int i, int wl, int n, const int s[4], double z,
-                              const FieldRec &r) {
+__device__ inline void put_xc(const SweepArgs &A, const FleetOut &O, int64_t inst, int M, int i, int wl, int n,
+                              const int s[4], double z, const FieldRec &r) {
     if (!(A.outs & kOutXC)) return;
     const int64_t at = xc_at(A, inst);
     if (at < 0) return;
     const Dev d = r.dev();
     if (A.outs & kOutX) {
-        double *x = A.out.x + at;
+        double *x = O.x + at;
         x[i] = double(wl); x[M + i] = double(n);
         x[2 * M + i] = double(s[0]); x[3 * M + i] = double(s[1]); x[4 * M + i] = double(s[2]);
         x[5 * M + i] = double(s[3]); x[6 * M + i] = z;
     }
     if (A.outs & kOutC) {
-        double *c = A.out.c + at;
+        double *c = O.c + at;
         c[i] = d.cw; c[M + i] = d.cn; c[2 * M + i] = d.cs0; c[3 * M + i] = d.cs1; c[4 * M + i] = d.cs2;
         c[5 * M + i] = d.cs3; c[6 * M + i] = 0.0;
     }
@@ -870,29 +874,41 @@ __device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
 // tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
 // only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
 // the one-fleet-per-wave table launch, as the register-only launch does.
-template <bool kTables, bool kGlobal, class SG = Wave>
-__device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const SG &sg) {
+// The steps kernel's prefetched fleet: the fields of the lane's device (loaded while the wave solved the
+// previous fleet), the fleet's first device, and the lane's k_j / W_j (loaded once per wave).
+struct SweepPre {
+    DevFields mf;
+    int64_t d0;
+    int kj, Wj;
+};
+
+// F / O: the batch's table and results (the kernel arguments' A.F / A.out, or one batch of a steps
+// launch); kPre: the fleet's fields come prefetched in *pre (every fleet has A.uM <= kK1MaxM devices).
+template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false>
+__device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const FleetOut &O, int f, const WaveCtx &w,
+                            const SG &sg, const SweepPre *pre = nullptr) {
     constexpr int S = SG::S;
     constexpr bool kSeg = S < 64;
     constexpr bool kFirst = !kTables || kSeg;  // a first launch: flags what it leaves to the table launch
     const int lane = sg.sl;  // device index within the fleet
     const SweepModel &Mo = A.Mo;
-    const halda_fleets &F = A.F;
     HALDA_SSTAMP(0, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(7, __builtin_amdgcn_s_memrealtime());
     // lane j: k_j and W_j = L / k_j (kernel arguments; their loads are issued with the fields')
     const bool kl = lane < A.n_k;
-    const int kj = A.ks[kl ? lane : 0];
-    const int Wj = kl ? A.Ws[lane] : 0;
+    const int kj = kPre ? pre->kj : A.ks[kl ? lane : 0];
+    const int Wj = kPre ? pre->Wj : kl ? A.Ws[lane] : 0;
     // the fleet's extent: with one fleet size for the batch, from dev_off[0] read through the scalar
     // cache (the table is read-only to the kernel), so that the field loads are the wave's first
     // vector round trip
     // with one fleet size for the batch the first device is dev_off[0] + f uM; dev_off[0] (0 in the
     // usual table) is read beside the field loads below, not in front of them
-    int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM : F.dev_off[f];
-    const int M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
+    int64_t d0 = kPre ? pre->d0 : A.uM > 0 ? int64_t(f) * A.uM : F.dev_off[f];
+    const int M = kPre ? A.uM : A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
+    // the outputs this call writes (a steps launch has no x / c: those paths compile out of it)
+    const int outs = kPre ? A.outs & (kOutObk | kOutSt) : A.outs;
     bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
-    if constexpr (kSeg) regs = true;  // the host sends fleets of at most S devices
+    if constexpr (kSeg || kPre) regs = true;  // the host sends fleets of at most S / kK1MaxM devices
     FieldRec me = {};
     int bad = 0;
     double tsum = 0.0, xsum = 0.0, kappa = 0.0;
@@ -901,8 +917,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         // fleet size the loads are issued at once from dev_off[0] = 0 (the usual table) while the
         // scalar read of dev_off[0] is in flight, and reissued only where it is not 0: no dependent
         // round trip in front of the field loads.
-        DevFields mf = load_fields(F, d0 + (lane < M ? lane : 0));
-        if (A.uM > 0) {
+        DevFields mf = kPre ? pre->mf : load_fields(F, d0 + (lane < M ? lane : 0));
+        if (!kPre && A.uM > 0) {
             // a vector read (returns in order behind the field loads: no wait of its own, unlike a
             // scalar read, whose lgkmcnt wait would also hold the kernel-argument reads)
             const int64_t base = __builtin_amdgcn_readfirstlane(int(F.dev_off[0])) |
@@ -930,7 +946,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     if constexpr (!kTables && !kSeg) {
         const double sink = me.alpha + me.b + me.p_bp + me.p_b + me.cst + double(me.Kset + me.Kvram + me.cls + me.gpu) +
                             tsum + xsum + kappa + double(bad);
-        if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+        if (lane == 0) O.obj_value[f] = sg.sum_f64(sink);
         return;
     }
 #endif
@@ -947,10 +963,10 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
     else if (M > 0 && bad) stj = HALDA_STATUS_UNSUPPORTED;
     if (kl && stj != kOpen) {
         const int64_t inst = int64_t(f) * A.n_k + lane;
-        if (A.outs & kOutObk) A.out.obj_by_k[inst] = kInf;
-        if (A.outs & kOutSt) A.out.status[inst] = stj;
+        if (outs & kOutObk) O.obj_by_k[inst] = kInf;
+        if (outs & kOutSt) O.status[inst] = stj;
     }
-    if ((A.outs & kOutXZ) && (A.outs & kOutXC)) {  // x / c of a settled instance are zero
+    if ((outs & kOutXZ) && (outs & kOutXC)) {  // x / c of a settled instance are zero
         uint64_t settled = sg.bits(kl && stj != kOpen);
         const int N = 7 * M + 1;
         while (settled) {
@@ -959,8 +975,8 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             const int64_t at = xc_at(A, int64_t(f) * A.n_k + j);
             if (at >= 0)
                 for (int cc = lane; cc < N; cc += S) {
-                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
-                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
+                    if (outs & kOutX) O.x[at + cc] = 0.0;
+                    if (outs & kOutC) O.c[at + cc] = 0.0;
                 }
         }
     }
@@ -993,7 +1009,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
             if constexpr (!kTables && !kSeg) {
                 const double sink = me.alpha + me.b + me.p_bp + me.p_b + me.cst + double(me.Kset + me.Kvram + me.cls +
                                     me.gpu + me.W + k + W) + tsum + xsum + kappa;
-                if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+                if (lane == 0) O.obj_value[f] = sg.sum_f64(sink);
                 return;
             }
 #endif
@@ -1015,7 +1031,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
 #if defined(HALDA_EXIT_AT) && HALDA_EXIT_AT == 3  // diagnostic: ... + the k = 1 greedy
             if constexpr (!kTables && !kSeg) {
                 const double sink = gE + double(e + nE + rounds + rc) + tsum + xsum + kappa;
-                if (lane == 0) A.out.obj_value[f] = sg.sum_f64(sink);
+                if (lane == 0) O.obj_value[f] = sg.sum_f64(sink);
                 return;
             }
 #endif
@@ -1028,7 +1044,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 // the cycle times only matter through (k - 1) max H and the x output: at k = 1 without x
                 // the largest cycle time is not formed (kc * hmax is +0 either way: hmax is finite and
                 // >= 0 after a successful split)
-                const bool need_h = kc != 0.0 || (A.outs & kOutX);
+                const bool need_h = kc != 0.0 || (outs & kOutX);
                 if (lane < M) {
                     if (haveE) {
                         g = gE;
@@ -1052,16 +1068,16 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 st = HALDA_STATUS_OPTIMAL;
                 improved = obj < best;
                 if (lane < M) {
-                    put_xc(A, inst, M, lane, wl, n, sl, z, me);
+                    if (outs & kOutXC) put_xc(A, O, inst, M, lane, wl, n, sl, z, me);
                     if (improved) {
-                        A.out.w[d0 + lane] = wl;
-                        A.out.n[d0 + lane] = n;
+                        O.w[d0 + lane] = wl;
+                        O.n[d0 + lane] = n;
                     }
                 }
-                if (lane == 0 && (A.outs & kOutXC)) {
+                if (lane == 0 && (outs & kOutXC)) {
                     const int64_t at = xc_at(A, inst);
-                    if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
-                    if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
+                    if (at >= 0 && (outs & kOutX)) O.x[at + 7 * M] = hmax;
+                    if (at >= 0 && (outs & kOutC)) O.c[at + 7 * M] = kc;
                 }
                 HALDA_SSTAMP(4, __builtin_amdgcn_s_memtime());
             } else if constexpr (!kTables) {
@@ -1083,7 +1099,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                 I.iC = 7 * M;
                 I.R1 = W - M + 1;
                 I.RS = odd_stride(I.R1);
-                const FieldSrc src{&A.Mo, &A.F, regs ? &me : nullptr, d0, W, sg.base};
+                const FieldSrc src{&A.Mo, &F, regs ? &me : nullptr, d0, W, sg.base};
                 int64_t nodes = 0;
                 const bool too_large =
                     M > A.mmax || I.R1 > A.r1max || int64_t(M) * I.RS > (kc > 0.0 ? A.tab_kc : A.tab);
@@ -1126,7 +1142,7 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                             dev_cycle(d, wl, n, sl, P, Q);
                             gs += g;
                             hmax = fmax(hmax, Q >= P ? 0.5 * (P + Q) : P);
-                            put_xc(A, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
+                            if (outs & kOutXC) put_xc(A, O, inst, M, i, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, d);
                         }
                     }
                     hmax = sg.max_f64(hmax);
@@ -1146,14 +1162,14 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
                                 double g;
                                 int n = 0, sl[4];
                                 split_full(d, wl, g, n, sl);
-                                A.out.w[d0 + i] = wl;
-                                A.out.n[d0 + i] = n;
+                                O.w[d0 + i] = wl;
+                                O.n[d0 + i] = n;
                             }
                         }
-                    if (lane == 0 && (A.outs & kOutXC)) {
+                    if (lane == 0 && (outs & kOutXC)) {
                         const int64_t at = xc_at(A, inst);
-                        if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
-                        if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
+                        if (at >= 0 && (outs & kOutX)) O.x[at + 7 * M] = hmax;
+                        if (at >= 0 && (outs & kOutC)) O.c[at + 7 * M] = kc;
                     }
                     HALDA_TSTAMP(8);
                 }
@@ -1163,40 +1179,40 @@ __device__ void sweep_fleet(const SweepArgs &A, int f, const WaveCtx &w, const S
         if (st == HALDA_STATUS_OPTIMAL && M == 0) {
             obj = 0.0;  // c.x = 0; no devices: the offsets are empty sums and kappa is undefined
             improved = obj < best;
-            if (lane == 0 && (A.outs & kOutXC)) {
+            if (lane == 0 && (outs & kOutXC)) {
                 const int64_t at = xc_at(A, inst);
-                if (at >= 0 && (A.outs & kOutX)) A.out.x[at] = 0.0;
-                if (at >= 0 && (A.outs & kOutC)) A.out.c[at] = kc;
+                if (at >= 0 && (outs & kOutX)) O.x[at] = 0.0;
+                if (at >= 0 && (outs & kOutC)) O.c[at] = kc;
             }
         }
         if (improved) {
             best = obj;
             best_k = k;
         }
-        if ((A.outs & kOutXZ) && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
+        if ((outs & kOutXZ) && st != HALDA_STATUS_OPTIMAL) {  // x / c of a non-optimal instance are zero
             const int N = 7 * M + 1;
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = lane; cc < N; cc += S) {
-                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
-                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
+                    if (outs & kOutX) O.x[at + cc] = 0.0;
+                    if (outs & kOutC) O.c[at + cc] = 0.0;
                 }
         }
         if (lane == 0) {
-            if (A.outs & kOutObk) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
-            if (A.outs & kOutSt) A.out.status[inst] = st;
+            if (outs & kOutObk) O.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (outs & kOutSt) O.status[inst] = st;
         }
     }
     HALDA_SSTAMP(5, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
-        A.out.best_k[f] = best_k;
-        A.out.obj_value[f] = best;
+        O.best_k[f] = best_k;
+        O.obj_value[f] = best;
         if (kFirst && A.fflag) A.fflag[f] = 0;
     }
     if (best_k == 0)
         for (int i = lane; i < M; i += S) {
-            A.out.w[d0 + i] = 0;
-            A.out.n[d0 + i] = 0;
+            O.w[d0 + i] = 0;
+            O.n[d0 + i] = 0;
         }
     HALDA_SSTAMP(6, __builtin_amdgcn_s_memtime());
     HALDA_SSTAMP(8, __builtin_amdgcn_s_memrealtime());
@@ -1232,7 +1248,7 @@ __device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base)
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            sweep_fleet<kTables, kGlobal>(A, int(b + int64_t(bit) * S), w, Wave(lane));
+            sweep_fleet<kTables, kGlobal>(A, A.F, A.out, int(b + int64_t(bit) * S), w, Wave(lane));
         }
     }
 }
@@ -1266,7 +1282,122 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
     __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
-    sweep_fleet<false, false>(A, f, w, Wave(int(threadIdx.x & 63)));
+    sweep_fleet<false, false>(A, A.F, A.out, f, w, Wave(int(threadIdx.x & 63)));
+}
+
+// ---------------------------------------------------------------- steps launch
+// halda_sweep_steps_kernel: `steps` consecutive batches of register sweeps (halda_fleets_group_launch)
+// in ONE launch. Batch t is group entry (first + t) mod n_desc: its own resident table and result
+// arrays, so every batch's outputs are those its own halda_sweep_kernel launch writes (the same
+// sweep_fleet code on the same fields). The waves stay resident: wave g takes fleets g, g + n_waves, ...
+// and, per fleet, the batches in order (a fleet's results in one batch are written by one wave, in
+// batch order, as consecutive launches would), and issues the field loads of its next (fleet, batch)
+// before it solves the current one, so the memory round trip of one item overlaps the compute of the
+// previous: no per-batch fill (every wave loading at once, then every wave computing) and no launch
+// per batch. Every batch shares the shape of the first (n_fleets, uM <= kK1MaxM devices, the model, the
+// k list, no x / c outputs): the host checks it.
+struct StepsDesc {
+    halda_fleets F;
+    FleetOut out;
+    int64_t base;  // dev_off[0] of the batch's table (read once by the host)
+};
+
+struct StepsArgs {
+    const StepsDesc *desc;
+    int n_desc;
+    int first;  // (first item's batch) mod n_desc
+    int steps;
+};
+
+__device__ inline const __attribute__((address_space(4))) StepsDesc &steps_desc(const StepsArgs &G, int b) {
+    return reinterpret_cast<const __attribute__((address_space(4))) StepsDesc *>(uintptr_t(G.desc))[b];
+}
+
+__device__ inline halda_fleets steps_fleets(const __attribute__((address_space(4))) StepsDesc &d) {
+    halda_fleets F;
+    F.n_fleets = d.F.n_fleets; F.min_devices = d.F.min_devices; F.max_devices = d.F.max_devices;
+    F.dev_off = d.F.dev_off; F.os_class = d.F.os_class; F.flags = d.F.flags;
+    F.scpu_b1 = d.F.scpu_b1; F.sgpu_b1 = d.F.sgpu_b1; F.T_cpu = d.F.T_cpu; F.T_gpu = d.F.T_gpu;
+    F.t_kvcpy_cpu = d.F.t_kvcpy_cpu; F.t_kvcpy_gpu = d.F.t_kvcpy_gpu; F.t_ram2vram = d.F.t_ram2vram;
+    F.t_vram2ram = d.F.t_vram2ram; F.t_comm = d.F.t_comm; F.s_disk = d.F.s_disk;
+    F.d_avail_ram = d.F.d_avail_ram; F.c_cpu = d.F.c_cpu; F.c_gpu = d.F.c_gpu; F.d_avail_cuda = d.F.d_avail_cuda;
+    F.d_avail_metal = d.F.d_avail_metal; F.swap = d.F.swap;
+    return F;
+}
+
+__device__ inline FleetOut steps_out(const __attribute__((address_space(4))) StepsDesc &d) {
+    FleetOut o;
+    o.best_k = d.out.best_k; o.obj_value = d.out.obj_value; o.w = d.out.w; o.n = d.out.n;
+    o.obj_by_k = d.out.obj_by_k; o.status = d.out.status; o.x = d.out.x; o.c = d.out.c;
+    return o;
+}
+
+// No instruction: every field is used (its load awaited) and redefined for the optimiser.
+__device__ inline void settle_fields(DevFields &f) {
+    asm volatile("" : "+v"(f.scpu), "+v"(f.sgpu), "+v"(f.Tc), "+v"(f.Tg), "+v"(f.tkc), "+v"(f.tkg), "+v"(f.r2v),
+                 "+v"(f.v2r), "+v"(f.tcomm), "+v"(f.sdisk));
+    asm volatile("" : "+v"(f.ram), "+v"(f.ccpu), "+v"(f.cgpu), "+v"(f.cuda), "+v"(f.metal), "+v"(f.swap), "+v"(f.cls),
+                 "+v"(f.flags));
+}
+
+#ifndef HALDA_STEPS_PREFETCH
+#define HALDA_STEPS_PREFETCH 1  // steps kernel: the next item's fields loaded while the current one is solved
+#endif
+#ifndef HALDA_STEPS_WAVES
+#define HALDA_STEPS_WAVES HALDA_SWEEP_WAVES_PER_SIMD
+#endif
+
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void halda_sweep_steps_kernel(
+    SweepArgs A, StepsArgs G) {
+    const int gw = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
+    const int nw = int(gridDim.x) * kSweepWavesPerBlock;
+    const int lane = int(threadIdx.x & 63);
+    const int nf = A.F.n_fleets, M = A.uM;
+    int f = gw;
+    if (f >= nf || G.steps <= 0) return;
+    __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
+    WaveCtx w = {};
+    w.dparg = dparg[threadIdx.x >> 6];
+    const Wave wv(lane);
+    SweepPre cur, nxt;
+    {
+        const bool kl = lane < A.n_k;
+        cur.kj = nxt.kj = A.ks[kl ? lane : 0];
+        cur.Wj = nxt.Wj = kl ? A.Ws[lane] : 0;
+    }
+    const int dl = lane < M ? lane : 0;
+    int t = 0, b = G.first;
+    cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
+    cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
+    // the first fields are awaited here: in the loop the wait for an item's fields is the one at the end
+    // of the previous item, never one that also waits for the loads issued for the next item
+    settle_fields(cur.mf);
+    while (true) {
+        // the next item: the same fleet's next batch, else the wave's next fleet from the first batch
+        int f2 = f, t2 = t + 1, b2 = b + 1 == G.n_desc ? 0 : b + 1;
+        if (t2 == G.steps) {
+            t2 = 0;
+            b2 = G.first;
+            f2 = f + nw;
+        }
+        const bool more = f2 < nf;
+        if (HALDA_STEPS_PREFETCH && more) {
+            nxt.d0 = steps_desc(G, b2).base + int64_t(f2) * M;
+            nxt.mf = load_fields(steps_fleets(steps_desc(G, b2)), nxt.d0 + dl);
+        }
+        sweep_fleet<false, false, Wave, true>(A, steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), f, w,
+                                              wv, &cur);
+        if (!more) break;
+        f = f2;
+        t = t2;
+        b = b2;
+        if (HALDA_STEPS_PREFETCH) {
+            cur = nxt;
+        } else {
+            cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
+            cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
+        }
+    }
 }
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
@@ -1309,7 +1440,7 @@ __global__ __launch_bounds__(64, HALDA_SEG_WAVES_PER_SIMD) void halda_sweep_seg_
     const int nf = A.F.n_fleets;
     for (int64_t b = int64_t(blockIdx.x) * kPer; b < nf; b += int64_t(gridDim.x) * kPer) {
         const int64_t f = b + seg;
-        if (f < nf) sweep_fleet<true, false, Seg<kSegLanes>>(A, int(f), w, sg);
+        if (f < nf) sweep_fleet<true, false, Seg<kSegLanes>>(A, A.F, A.out, int(f), w, sg);
     }
 }
 
@@ -1554,7 +1685,7 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
                 obj = obj + kappa;
                 st = HALDA_STATUS_OPTIMAL;
                 nl = n;
-                if (lane < M) put_xc(A, inst, M, lane, wl, n, sl, z, me);
+                if (lane < M) put_xc(A, A.out, inst, M, lane, wl, n, sl, z, me);
                 if (lane == 0 && (A.outs & kOutXC)) {
                     const int64_t at = xc_at(A, inst);
                     if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
@@ -1597,7 +1728,7 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
                         split_full(me, wl, g, n, sl);
                         dev_cycle(me, wl, n, sl, P, Q);
                         hmax = Q >= P ? 0.5 * (P + Q) : P;
-                        put_xc(A, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
+                        put_xc(A, A.out, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
                     }
                     hmax = sg.max_f64(fmax(0.0, hmax));
                     obj = sg.sum_f64(0.0 + g) + kc * hmax;  // the segment kernel's sum (0.0 + g per lane)

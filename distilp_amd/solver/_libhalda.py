@@ -82,7 +82,8 @@ EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batc
            "halda_last_fleet_ms", "halda_set_fleets_path", "halda_init_multi", "halda_solve_fleets_multi",
            "halda_free_multi", "halda_comm_unique_id", "halda_comm_init", "halda_comm_destroy",
            "halda_solve_fleets_sharded", "halda_fleets_plan_create", "halda_fleets_plan_launch",
-           "halda_fleets_plan_free", "halda_solve_fleets_sharded_emulated", "halda_fleets_plan_launch_many")
+           "halda_fleets_plan_free", "halda_solve_fleets_sharded_emulated", "halda_fleets_plan_launch_many",
+           "halda_fleets_group_create", "halda_fleets_group_launch", "halda_fleets_group_free")
 
 _lib = None
 _lib_lock = threading.Lock()

@@ -111,6 +111,13 @@ def _bind(lib):
                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int64,
                                                   ctypes.c_int32]
     lib.halda_fleets_plan_launch_many.restype = ctypes.c_int
+    lib.halda_fleets_group_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
+                                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int32)]
+    lib.halda_fleets_group_create.restype = ctypes.c_int
+    lib.halda_fleets_group_launch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+    lib.halda_fleets_group_launch.restype = ctypes.c_int
+    lib.halda_fleets_group_free.argtypes = [ctypes.c_void_p]
+    lib.halda_fleets_group_free.restype = None
     lib._fleets_bound = True
     return lib
 
@@ -666,6 +673,7 @@ class DeviceFleetTable:
                                      o["status"].data_ptr() if want_per_k else None, None, None)
         self.model = model_struct(model, kv_factor)
         self._plans = {}
+        self.epoch = 0  # bumped whenever the prepared plans are freed (PlanRotation re-reads the handles)
 
     def nbytes(self) -> int:
         return sum(int(t.numel() * t.element_size()) for t in self.arrs.values())
@@ -674,7 +682,11 @@ class DeviceFleetTable:
         """The prepared launch of this table on `ctx` (halda_fleets_plan_create: kernel choice, grids and
         kernel arguments derived once), created on first use and kept with the table (a set_fleets_path
         on ctx re-plans it at its next launch)."""
+        if getattr(ctx, "ctx", None) is None:
+            raise RuntimeError("DeviceFleetTable.plan: the context is closed")
         p = self._plans.get(id(ctx))
+        if p is not None and p[0] is not ctx:  # a new context at a recycled id()
+            p = None
         if p is None:
             lib = _bind(ctx.lib)
             h = ctypes.c_void_p()
@@ -689,10 +701,12 @@ class DeviceFleetTable:
         return p
 
     def replan(self) -> None:
-        """Free the prepared launches (the next launch prepares a new one)."""
+        """Free the prepared launches (the next launch prepares a new one). A PlanRotation over this
+        table takes the new handles at its next launch; a PlanGroup keeps its own copy."""
         for ctx, h, _ in self._plans.values():
             _bind(ctx.lib).halda_fleets_plan_free(h)
         self._plans.clear()
+        self.epoch += 1
 
     def __del__(self):  # pragma: no cover - interpreter shutdown order
         try:
@@ -703,7 +717,8 @@ class DeviceFleetTable:
     def launch(self, ctx, stream: int) -> None:
         """Enqueue one k-sweep of every fleet on `stream` (a hipStream_t as int) through the prepared
         plan: one ctypes call, one or two kernel enqueues."""
-        c, h, fn = self._plans.get(id(ctx)) or self.plan(ctx)
+        p = self._plans.get(id(ctx))
+        c, h, fn = p if p is not None and p[0] is ctx and ctx.ctx is not None else self.plan(ctx)
         with ctx._lock:
             rc = fn(h, stream)
         if rc != 0:
@@ -758,19 +773,65 @@ class PlanRotation:
     per batch."""
 
     def __init__(self, tables, ctx, streams):
-        plans = [t.plan(ctx)[1] for t in tables]
         self.ctx = ctx
         self.lib = _bind(ctx.lib)
-        self.n_p, self.n_s = len(plans), len(streams)
-        self.plans = (ctypes.c_void_p * self.n_p)(*[p.value for p in plans])
+        self.tables = list(tables)  # (the plans live with them)
+        self.n_p, self.n_s = len(self.tables), len(streams)
         self.streams = (ctypes.c_void_p * self.n_s)(*[ctypes.c_void_p(int(x)).value for x in streams])
-        self.tables = tables  # (the plans live with them)
+        self._take_plans()
+
+    def _take_plans(self) -> None:
+        self.plans = (ctypes.c_void_p * self.n_p)(*[t.plan(self.ctx)[1].value for t in self.tables])
+        self.epochs = [t.epoch for t in self.tables]
 
     def launch(self, first: int, steps: int) -> None:
+        if self.ctx.ctx is None:
+            raise RuntimeError("PlanRotation.launch: the context is closed")
+        if [t.epoch for t in self.tables] != self.epochs:  # a table re-planned: its old handle is freed
+            self._take_plans()
         with self.ctx._lock:
             rc = self.lib.halda_fleets_plan_launch_many(self.plans, self.n_p, self.streams, self.n_s, first, steps)
         if rc != 0:
             raise RuntimeError(f"halda_fleets_plan_launch_many failed ({rc}): {last_error(self.lib)}")
+
+
+class PlanGroup:
+    """Resident tables run as a stream of batches by ONE launch (halda_fleets_group_launch): batch t of
+    launch(first, steps, stream) is table (first + t) % len(tables), each batch's results in its own
+    table's arrays, as PlanRotation over one stream would leave them. `persistent` tells whether the
+    steps run as one launch (register sweeps of one shape: C3) or batch by batch."""
+
+    def __init__(self, tables, ctx):
+        self.ctx = ctx
+        self.lib = _bind(ctx.lib)
+        self.tables = list(tables)  # the group reads their device arrays: they stay alive with it
+        plans = (ctypes.c_void_p * len(self.tables))(*[t.plan(ctx)[1].value for t in self.tables])
+        self.group = ctypes.c_void_p()
+        pers = ctypes.c_int32(0)
+        with ctx._lock:
+            rc = self.lib.halda_fleets_group_create(plans, len(self.tables), ctypes.byref(self.group), ctypes.byref(pers))
+        if rc != 0:
+            raise RuntimeError(f"halda_fleets_group_create failed ({rc}): {last_error(self.lib)}")
+        self.persistent = bool(pers.value)
+
+    def launch(self, first: int, steps: int, stream: int) -> None:
+        if self.ctx.ctx is None:
+            raise RuntimeError("PlanGroup.launch: the context is closed")
+        with self.ctx._lock:
+            rc = self.lib.halda_fleets_group_launch(self.group, first, steps, ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"halda_fleets_group_launch failed ({rc}): {last_error(self.lib)}")
+
+    def close(self) -> None:
+        if getattr(self, "group", None):
+            self.lib.halda_fleets_group_free(self.group)
+            self.group = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def launch_sharded_emulated(dt: "DeviceFleetTable", ctx, world: int, report_rank: int, stream: int) -> None:

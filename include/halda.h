@@ -127,9 +127,8 @@ int halda_last_solve_kernel_ms(void *ctx, double *ms);
  * off drops four event records per launch from the stream. */
 int halda_set_timing(void *ctx, int on);
 
-/* Device time of the last solve per launch, in ms: ms3[0] the screen + k = 1
- * kernel (halda_screen_k1_kernel; with HALDA_TWO_PASS=1 in the environment the
- * screen kernel alone), ms3[1] 0 (two-pass: the persistent k = 1 kernel),
+/* Device time of the last solve per launch, in ms: ms3[0] the screen kernel
+ * (halda_screen_kernel), ms3[1] the persistent k = 1 kernel (halda_solve_k1_kernel),
  * ms3[2] the general kernel's launches (k > 1, then k = 1 wide / hand-backs). */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
@@ -221,6 +220,21 @@ int halda_fleets_plan_launch(void *plan, void *stream);
 int halda_fleets_plan_launch_many(void *const *plans, int32_t n_plans, void *const *streams, int32_t n_streams,
                                   int64_t first, int32_t steps);
 void halda_fleets_plan_free(void *plan);
+
+/* A group of prepared plans run as a stream of batches: halda_fleets_group_launch(group, first, steps,
+ * stream) solves batch t = plans[(first + t) % n_plans] for t = 0 .. steps - 1, each batch's results in
+ * its own plan's arrays, exactly as halda_fleets_plan_launch_many(plans, n_plans, &stream, 1, first,
+ * steps) would leave them. When every plan is a register sweep of one shape (the same model, k list,
+ * fleet count and fleet size uM <= 64, no x / c outputs: C3's resident copies) the steps run as ONE
+ * launch whose resident waves load each next (fleet, batch)'s fields while solving the current one
+ * (*persistent = 1); otherwise batch by batch on `stream` (*persistent = 0). The group copies what it
+ * needs from the plans at creation (the plans may be freed after it); the tables and result arrays
+ * behind them must stay allocated while the group lives. Plans and groups fail with HALDA_E_ARG once
+ * their context was freed. Replaces the per-batch loop over halda_solve (halda_p_solver.py:369-436)
+ * that a streaming caller runs. */
+int halda_fleets_group_create(void *const *plans, int32_t n_plans, void **group, int32_t *persistent);
+int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *stream);
+void halda_fleets_group_free(void *group);
 
 /* How halda_solve_fleets runs (default 1; HALDA_FLEETS_PATH=csr / =wave at halda_init select 0 / 2):
  * 1 the fused sweep (halda_sweep_kernel: every (fleet, k) built in registers from the device

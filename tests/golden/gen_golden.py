@@ -15,6 +15,15 @@ inputs and outputs (data) are written:
   tests/golden/synthetic_M{M}.json   seeded fleets (device dicts) + per-k results
   tests/golden/lowered.npz           the exact MILP arrays (c, A_ub CSR, b_ub, A_eq,
                                      bounds, integrality) for a few (fleet, k)
+  tests/golden/ties.json             fleets of repeated devices (exact ties): the
+                                     reference's own "same device twice" shape
+                                     (test/test_integration.py:88, loaded by its
+                                     cli.solver.load_devices_and_model) for every
+                                     profile folder x kv_bits x mip_gap, and the tied
+                                     synthetic fleets of tests/ties.py (copies / two /
+                                     half) under two models: HALDAResult + per-k
+
+Run `python tests/golden/gen_golden.py ties` to (re)write ties.json alone.
 
 Solver: scipy 1.15.3 / HiGHS 1.8.0 (git 222cce7), the version present here.
 """
@@ -205,5 +214,64 @@ def main():
     np.savez_compressed(HERE / "lowered.npz", **lowered)
 
 
+TIE_SEED0, TIE_N_EACH = 21000, 20  # tests/ties.py tied_fleets(20): 60 fleets
+TIE_MODELS = {"llama_3_70b/online": None, "qwen3_32b/bf16": "test/profiles/qwen3_32b/bf16/model_profile.json"}
+
+
+def tied_fleet_dicts(synth_fleet, tpl):
+    """[(kind, seed, device dicts)] built exactly as tests/ties.py tied_fleets() builds its fleets."""
+    import copy
+
+    out = []
+    for s in range(TIE_N_EACH):
+        src = synth_fleet(TIE_SEED0 + s, 16, tpl)
+        one = src[s % 2]
+        out.append(("copies", s, [copy.deepcopy(one) for _ in range(16)]))
+        out.append(("two", s, [copy.deepcopy(src[1]) for _ in range(8)] + [copy.deepcopy(src[2 + s % 14]) for _ in range(8)]))
+        out.append(("half", s, copy.deepcopy(src[:8] + src[:8])))
+    return out
+
+
+def gen_ties():
+    hp, cli, DeviceProfile, ModelProfileSplit = import_reference()
+    sys.path.append(str(REPO))
+    from distilp_amd.synth import load_model_dict, load_templates, synth_fleet  # our generator (data only)
+
+    os.chdir(REF_ROOT)
+    t0 = time.time()
+    twice = {}
+    for folder in FOLDERS:
+        base = Path("test/profiles") / folder
+        dev = sorted(p for p in base.glob("*.json") if p.name != "model_profile.json")[0]
+        devs, model = cli.load_devices_and_model([str(dev), str(dev)], str(base / "model_profile.json"))
+        for kv in KV:
+            for gap in GAPS:
+                res, err, calls, _ = run_solve(hp, devs, model, kv, gap)
+                twice[f"{folder}|{kv}|{gap:g}"] = {"folder": folder, "device_file": dev.name, "kv_bits": kv,
+                                                   "mip_gap": gap, "result": res, "error": err,
+                                                   "per_k": strip_arrays(calls)}
+    print(f"twice done {time.time() - t0:.1f}s", file=sys.stderr)
+    tpl = load_templates()
+    fleets = tied_fleet_dicts(synth_fleet, tpl)
+    tied = {}
+    for mname, mfile in TIE_MODELS.items():
+        if mfile is None:
+            model = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+        else:
+            model = cli.load_model_profile(mfile)
+        rows = []
+        for kind, seed, dicts in fleets:
+            devs = [DeviceProfile.model_validate(d) for d in dicts]
+            res, err, calls, _ = run_solve(hp, devs, model, "4bit", 1e-4)
+            rows.append({"kind": kind, "seed": seed, "result": res, "error": err, "per_k": strip_arrays(calls)})
+        tied[mname] = {"model": mname, "kv_bits": "4bit", "mip_gap": 1e-4, "fleets": rows}
+        print(f"tied {mname} done {time.time() - t0:.1f}s", file=sys.stderr)
+    (HERE / "ties.json").write_text(json.dumps({"twice": twice, "tied": tied, "seed0": TIE_SEED0,
+                                                "n_each": TIE_N_EACH}))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ties"]:
+        gen_ties()
+    else:
+        main()

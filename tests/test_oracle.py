@@ -128,3 +128,33 @@ def test_exact_oracle_matches_highs_with_zero_w_bounds(llama_online_model):
         assert (st == 0) == (r.status == 0), (k, nz, st, r.status)
         if st == 0:
             assert abs(b1 - r.fun) <= 1e-9 * max(1.0, abs(r.fun)), (k, nz, b1, r.fun)
+
+
+def test_oracle_matches_reference_tie_goldens():
+    """tests/golden/ties.json -- the reference itself run on fleets of repeated devices (the "same device
+    twice" shape of test/test_integration.py:88 for every folder x kv_bits x mip_gap, and tied synthetic
+    fleets under two models): the oracle's HiGHS path returns the reference's HALDAResult bit for bit
+    (the same lowering, scipy and HiGHS), and the exact C solver's sweep lies inside what HiGHS proved
+    per k (check_sweep_against_golden). This pins the oracle on ties, where test_gpu_ties.py checks the GPU."""
+    from .ties import TIE_MODELS, check_sweep_against_golden, tie_golden, tie_model, tied_fleets, twice_cases
+
+    for key, devs, model, kv, gap, g in twice_cases():
+        hi, _ = mo.halda_solve_oracle(devs, model, mip_gap=gap, kv_bits=kv, solver="highs")
+        assert hi == g["result"], key
+        ex, ek = mo.halda_solve_oracle(devs, model, mip_gap=gap, kv_bits=kv, solver="exact")
+        check_sweep_against_golden(g, {r["k"]: (r["obj_value"] if r["success"] else None) for r in ek}, ex["k"],
+                                   ex["obj_value"])
+    gold = tie_golden()
+    fleets = tied_fleets(gold["n_each"], gold["seed0"])
+    for name in TIE_MODELS:
+        model = tie_model(name)
+        rows = gold["tied"][name]["fleets"]
+        assert len(rows) == len(fleets)
+        for i in range(0, len(fleets), 3):  # every third fleet through HiGHS (time), all through the exact solver
+            hi, _ = mo.halda_solve_oracle(fleets[i][1], model, mip_gap=1e-4, kv_bits="4bit", solver="highs")
+            assert hi == rows[i]["result"], (name, i)
+        for (kind, devs), row in zip(fleets, rows):
+            assert kind == row["kind"]
+            ex, ek = mo.halda_solve_oracle(devs, model, mip_gap=1e-4, kv_bits="4bit", solver="exact")
+            check_sweep_against_golden(row, {r["k"]: (r["obj_value"] if r["success"] else None) for r in ek},
+                                       ex["k"], ex["obj_value"])

@@ -46,3 +46,77 @@ def tied_fleets(n_each=20, seed0=21000):
         out.append(("two", _validate([src[1]] * 8 + [src[2 + s % 14]] * 8)))
         out.append(("half", _validate(src[:8] + src[:8])))
     return out
+
+
+# ---------------------------------------------------------------- reference-run goldens for ties
+# tests/golden/ties.json (tests/golden/gen_golden.py `ties`): the reference's halda_solve on the
+# "same device twice" shape (its own cli loader) for every folder x kv_bits x mip_gap, and on
+# tied_fleets(20) under two models; per k the HiGHS status, obj_value, fun and dual bound.
+TIE_MODELS = ("llama_3_70b/online", "qwen3_32b/bf16")
+
+
+def tie_golden():
+    import json
+
+    return json.loads((REPO / "tests" / "golden" / "ties.json").read_text())
+
+
+def twice_cases():
+    """[(key, devices, model, kv_bits, mip_gap, golden entry)] of the golden's twice cases."""
+    from distilp_amd.cli.solver import load_devices_and_model
+
+    out = []
+    for key, g in tie_golden()["twice"].items():
+        base = REPO / "test" / "profiles" / g["folder"]
+        dev = str(base / g["device_file"])
+        devs, model = load_devices_and_model([dev, dev], str(base / "model_profile.json"))
+        out.append((key, devs, model, g["kv_bits"], g["mip_gap"], g))
+    return out
+
+
+def tie_model(name):
+    """The model a tied-fleet golden was made with: the synthetic llama_3_70b/online profile, or the
+    qwen3_32b/bf16 folder's (loaded as the reference CLI loads it)."""
+    from distilp_amd.common import ModelProfileSplit
+    from distilp_amd.synth import load_model_dict
+
+    if name == "llama_3_70b/online":
+        return ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+    from distilp_amd.cli.solver import load_devices_and_model
+
+    base = REPO / "test" / "profiles" / name
+    dev = sorted(p for p in base.glob("*.json") if p.name != "model_profile.json")[0]
+    return load_devices_and_model([str(dev)], str(base / "model_profile.json"))[1]
+
+
+def _eps(v):
+    return 1e-9 * max(1.0, abs(v))
+
+
+def check_sweep_against_golden(g, ours_per_k, ours_k, ours_obj):
+    """One k-sweep against the reference's: g = {"result", "per_k"}; ours_per_k = {k: obj_value or None
+    (infeasible)}. Per k the same status and an objective inside the interval HiGHS proved
+    [obj_value - (fun - dual_bound), obj_value] (a point when HiGHS closed the gap); the best objective no
+    worse than the reference's, and the same best k wherever every k was closed and the reference's best
+    is unique by more than 1e-9. Returns True when the golden is exact (every gap closed)."""
+    exact = True
+    objs = []
+    for r in g["per_k"]:
+        o = ours_per_k[r["k"]]
+        if not r["success"]:
+            assert o is None, (r["k"], o)
+            continue
+        assert o is not None, r["k"]
+        hi = r["obj_value"]
+        gap = r["fun"] - r["dual_bound"]
+        exact = exact and gap <= _eps(r["fun"])
+        assert hi - max(gap, 0.0) - _eps(hi) <= o <= hi + _eps(hi), (r["k"], o, hi, gap)
+        objs.append(hi)
+    res = g["result"]
+    assert res is not None and ours_k > 0
+    assert ours_obj <= res["obj_value"] + _eps(res["obj_value"]), (ours_obj, res["obj_value"])
+    objs.sort()
+    if exact and (len(objs) < 2 or objs[1] - objs[0] > _eps(objs[0])):
+        assert ours_k == res["k"], (ours_k, res["k"])
+        assert abs(ours_obj - res["obj_value"]) <= _eps(res["obj_value"])
+    return exact

@@ -1,6 +1,8 @@
 """Diagnostic: C3 k-sweep timings of the library HALDA_LIB points at -- one launch (HIP events around 200
-back-to-back launches on one stream), the two-stream step (200 and 20 steps, wall, as bench.py's
-headline) -- for A/B runs of build variants:  HALDA_LIB=build/variants/x.so python tools/ab_c3.py [--M 64]"""
+back-to-back launches on one stream), the two-stream step (200 and 20 steps, wall), and the group launch
+of bench.py's headline (K batches in one halda_fleets_group_launch: wall per step at K = 200 and 20, and
+the launch's own HIP-event time) -- for A/B runs of build variants:
+    HALDA_LIB=build/variants/x.so python tools/ab_c3.py [--M 64]"""
 import json
 import os
 import sys
@@ -16,7 +18,7 @@ def main():
 
     import bench
     from distilp_amd.solver._libhalda import get_context
-    from distilp_amd.solver.fleets import DeviceFleetTable, fleet_table
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup, fleet_table
 
     M = int(sys.argv[sys.argv.index("--M") + 1]) if "--M" in sys.argv else 64
     dev = torch.device("cuda", 0)
@@ -43,6 +45,20 @@ def main():
             dts[i % 16].launch(ctx, ss[i % 2].cuda_stream)
         torch.cuda.synchronize(dev)
         out.setdefault(f"two_stream_{steps}_us", []).append((time.perf_counter() - t0) / steps * 1e6)
+    group = PlanGroup(dts, ctx)
+    out["persistent"] = group.persistent
+    group.launch(0, 20, ss[0].cuda_stream)
+    for steps in (200, 20, 200, 20):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        group.launch(0, steps, ss[0].cuda_stream)
+        torch.cuda.synchronize(dev)
+        out.setdefault(f"group_{steps}_us", []).append((time.perf_counter() - t0) / steps * 1e6)
+        e0.record(ss[0])
+        group.launch(0, steps, ss[0].cuda_stream)
+        e1.record(ss[0])
+        torch.cuda.synchronize(dev)
+        out.setdefault(f"group_{steps}_event_us_per_step", []).append(e0.elapsed_time(e1) / steps * 1e3)
     print(json.dumps(out), flush=True)
 
 
