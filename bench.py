@@ -408,20 +408,60 @@ def pmc_traffic(kernel):
 
 
 def time_to_optimal(model, M: int, runs: int = 100):
+    """Median wall ms of one M = 64 halda_solve (Python call -> HALDAResult), and its parts, each the
+    median of `runs` calls of that part alone (so they need not add up exactly): `pack` the C packer
+    (DeviceProfile objects -> the fleet's field table), `gpu_call` the synchronous libhalda call
+    (halda_solve_fleets_host: table across PCIe, the k-sweep kernel, results back) and the objective
+    constants, `rest` the total's median minus those two (k list, per-k results with NumPy's c.x, the
+    pick and HALDAResult). `gpu_call_copy_path`: the same call through explicit H2D / D2H copies instead
+    of the kernel reading and writing pinned host memory (a second context, HALDA_HOST_PATH=copy)."""
     import contextlib
     import io
 
     from distilp_amd.solver import halda_solve
+    from distilp_amd.solver._libhalda import HaldaContext
+    from distilp_amd.solver.fleets import _bind, model_struct, pack_one, sweep_one
 
     devs = build_fleets([0], M)[0]
-    times = []
-    for i in range(runs + 5):
-        t0 = time.perf_counter()
+
+    def med(fn):
+        ts = []
+        for i in range(runs + 5):
+            t0 = time.perf_counter()
+            fn()
+            if i >= 5:
+                ts.append((time.perf_counter() - t0) * 1e3)
+        return statistics.median(ts)
+
+    def one():
         with contextlib.redirect_stdout(io.StringIO()):
             halda_solve(devs, model, mip_gap=1e-4, plot=False, kv_bits="4bit")
-        if i >= 5:
-            times.append((time.perf_counter() - t0) * 1e3)
-    return statistics.median(times)
+
+    total = med(one)
+    ks = KS_L80
+    pack = med(lambda: pack_one(devs, model, ks))
+    ws = pack_one(devs, model, ks)
+    call = med(lambda: sweep_one(ws, model, 0.5))
+    parts = {"pack_ms": pack, "gpu_call_ms": call, "rest_ms": total - pack - call}
+    import ctypes
+
+    os.environ["HALDA_HOST_PATH"] = "copy"
+    try:
+        ctx2 = HaldaContext(0)
+    finally:
+        os.environ.pop("HALDA_HOST_PATH", None)
+    lib = _bind(ctx2.lib)
+    m = model_struct(model, 0.5)
+
+    def copy_call():
+        rc = lib.halda_solve_fleets_host(ctx2.ctx, ctypes.byref(m), ctypes.byref(ws.fs), ws.karr.ctypes.data,
+                                         len(ws.ks), ctypes.byref(ws.res))
+        if rc != 0:
+            raise RuntimeError("copy-path call failed")
+
+    parts["gpu_call_copy_path_ms"] = med(copy_call)
+    ctx2.close()
+    return total, parts
 
 
 def batch_api(model, fleets, runs: int = 3):
@@ -847,7 +887,7 @@ def main():
         c2 = c2_leg(args, torch, dev, ctx, model, stream, srefs)
         lat = None if args.no_latency else latency_leg(torch, dev, ctx, model, stream)
     if rank == 0:
-        tto = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else None
+        tto, tto_parts = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else (None, None)
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
         bapi = batch_api(model, fleets) if (world == 1 and not args.no_tto) else None
         line = {
@@ -893,6 +933,7 @@ def main():
             "feasible_instances_per_s": value * n_opt / batch.n_inst,
             "fleets_per_s": n_fleets_total / el_sweep,
             "time_to_optimal_ms": tto,
+            "time_to_optimal_parts": tto_parts,
             "roofline": group_roofline(group_ms, args.steps, alg["halda_sweep_kernel"], len(fleets),
                                        roofline(fl_mean, alg, pmc_traffic, sweep_ev_ms)),
             "solve_only": {

@@ -92,6 +92,7 @@ struct Ctx {
     bool seg_sweep = true;         // fused sweep: lane-segment launch for fleets of <= kSegLanes devices
     bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
     bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
+    bool host_copy = false;        // halda_solve_fleets_host: PCIe copies even for small calls (HALDA_HOST_PATH=copy)
     bool last_fleet_fused = false;
     int path_gen = 0;              // bumped by halda_set_fleets_path: prepared plans re-plan on their next launch
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
@@ -899,6 +900,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     const char *fp = std::getenv("HALDA_FLEETS_PATH");
     c->fleets_fused = !(fp && std::strcmp(fp, "csr") == 0);
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
+    const char *hp = std::getenv("HALDA_HOST_PATH");  // diagnostic A/B of the small synchronous call
+    c->host_copy = hp && std::strcmp(hp, "copy") == 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
@@ -1348,14 +1351,12 @@ int group_check(FleetsGroup *G) {
     if (!G->desc) HIP_TRY(hipMalloc(&G->desc, sizeof(StepsDesc) * h.size()));
     HIP_TRY(hipMemcpy(G->desc, h.data(), sizeof(StepsDesc) * h.size(), hipMemcpyHostToDevice));
     G->A = P0.p.A;
-    // every wave resident at once: the occupancy of the steps kernel (4 waves per SIMD) on every CU,
-    // at most one wave per fleet
+    // every wave resident at once: the occupancy of the steps kernel on every CU (the launch caps it at
+    // one wave per item)
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(halda_sweep_steps_kernel),
                                                          64 * kSweepWavesPerBlock, 0));
-    const int64_t waves = int64_t(std::max(per_cu, 1)) * c->cus * kSweepWavesPerBlock;
-    const int64_t need = (int64_t(P0.F.n_fleets) + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock;
-    G->grid = unsigned(std::max<int64_t>(1, std::min(waves / kSweepWavesPerBlock, need)));
+    G->grid = unsigned(std::max(per_cu, 1) * c->cus);
     G->persistent = true;
     return HALDA_OK;
 }
@@ -1421,7 +1422,9 @@ int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *s
     c->fleet_timed = false;
     c->have_lowered = false;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(G->grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
+    const int64_t items = int64_t(steps) * G->plans[0].F.n_fleets;
+    const unsigned grid = unsigned(std::min<int64_t>(G->grid, (items + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock));
+    hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
     HIP_TRY(hipGetLastError());
     if (c->timing) {
         HIP_TRY(hipEventRecord(c->evf1, s));
@@ -1521,7 +1524,7 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     // table from and write the results to the pinned buffer itself, across PCIe, and the host polls
     // the completion event instead of sleeping in a stream synchronisation
     if (xsel) HIP_TRY(up(o_xoff, out_h->x_off, 8 * size_t(nf) * n_k));
-    const bool zc = off <= kZeroCopyBytes;
+    const bool zc = off <= kZeroCopyBytes && !c->host_copy;
     if (zc) {
         void *dp = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));

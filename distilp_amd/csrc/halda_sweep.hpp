@@ -1289,13 +1289,17 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_SWEEP_WAVES_PER_SIM
 // halda_sweep_steps_kernel: `steps` consecutive batches of register sweeps (halda_fleets_group_launch)
 // in ONE launch. Batch t is group entry (first + t) mod n_desc: its own resident table and result
 // arrays, so every batch's outputs are those its own halda_sweep_kernel launch writes (the same
-// sweep_fleet code on the same fields). The waves stay resident: wave g takes fleets g, g + n_waves, ...
-// and, per fleet, the batches in order (a fleet's results in one batch are written by one wave, in
-// batch order, as consecutive launches would), and issues the field loads of its next (fleet, batch)
-// before it solves the current one, so the memory round trip of one item overlaps the compute of the
-// previous: no per-batch fill (every wave loading at once, then every wave computing) and no launch
-// per batch. Every batch shares the shape of the first (n_fleets, uM <= kK1MaxM devices, the model, the
-// k list, no x / c outputs): the host checks it.
+// sweep_fleet code on the same fields). The waves stay resident, six per SIMD (78 VGPRs): the items
+// (batch t, fleet f) are taken in batch order, wave g takes items g, g + n_waves, ..., so at any time
+// the resident waves work on one or two consecutive batches (neighbouring table rows in HBM) and a
+// wave waiting for its next fleet's fields leaves the SIMD to the five others. No per-batch fill
+// (every wave of a launch loading at once, then every wave computing) and no launch per batch.
+// Measured against the alternatives: register prefetch of the next item's fields
+// (116 VGPRs, four waves per SIMD), fleet-order items, staggered wave starts -- all slower.
+// A (batch, fleet) item that recurs (more batches than group entries) may be solved by two waves at
+// once: they compute the same values and every location's last write is the final value, so the
+// results are those of consecutive launches. Every batch shares the shape of the first (n_fleets,
+// uM <= kK1MaxM devices, the model, the k list, no x / c outputs): the host checks it.
 struct StepsDesc {
     halda_fleets F;
     FleetOut out;
@@ -1332,19 +1336,8 @@ __device__ inline FleetOut steps_out(const __attribute__((address_space(4))) Ste
     return o;
 }
 
-// No instruction: every field is used (its load awaited) and redefined for the optimiser.
-__device__ inline void settle_fields(DevFields &f) {
-    asm volatile("" : "+v"(f.scpu), "+v"(f.sgpu), "+v"(f.Tc), "+v"(f.Tg), "+v"(f.tkc), "+v"(f.tkg), "+v"(f.r2v),
-                 "+v"(f.v2r), "+v"(f.tcomm), "+v"(f.sdisk));
-    asm volatile("" : "+v"(f.ram), "+v"(f.ccpu), "+v"(f.cgpu), "+v"(f.cuda), "+v"(f.metal), "+v"(f.swap), "+v"(f.cls),
-                 "+v"(f.flags));
-}
-
-#ifndef HALDA_STEPS_PREFETCH
-#define HALDA_STEPS_PREFETCH 1  // steps kernel: the next item's fields loaded while the current one is solved
-#endif
 #ifndef HALDA_STEPS_WAVES
-#define HALDA_STEPS_WAVES HALDA_SWEEP_WAVES_PER_SIMD
+#define HALDA_STEPS_WAVES 6  // resident waves per SIMD of the steps kernel
 #endif
 
 __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void halda_sweep_steps_kernel(
@@ -1353,50 +1346,39 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void h
     const int nw = int(gridDim.x) * kSweepWavesPerBlock;
     const int lane = int(threadIdx.x & 63);
     const int nf = A.F.n_fleets, M = A.uM;
-    int f = gw;
-    if (f >= nf || G.steps <= 0) return;
+    if (G.steps <= 0 || nf <= 0) return;
+    // items in batch order, item i = (batch t = i / nf, fleet f = i % nf); wave g takes g, g + nw, ...
+    int f = gw % nf, t = gw / nf;
+    if (t >= G.steps) return;
+    int b = int((int64_t(G.first) + t) % G.n_desc);
+    const int dt = nw / nf, df = nw % nf, db = dt % G.n_desc;
     __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
     const Wave wv(lane);
-    SweepPre cur, nxt;
+    SweepPre cur;
     {
         const bool kl = lane < A.n_k;
-        cur.kj = nxt.kj = A.ks[kl ? lane : 0];
-        cur.Wj = nxt.Wj = kl ? A.Ws[lane] : 0;
+        cur.kj = A.ks[kl ? lane : 0];
+        cur.Wj = kl ? A.Ws[lane] : 0;
     }
     const int dl = lane < M ? lane : 0;
-    int t = 0, b = G.first;
-    cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
-    cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
-    // the first fields are awaited here: in the loop the wait for an item's fields is the one at the end
-    // of the previous item, never one that also waits for the loads issued for the next item
-    settle_fields(cur.mf);
     while (true) {
-        // the next item: the same fleet's next batch, else the wave's next fleet from the first batch
-        int f2 = f, t2 = t + 1, b2 = b + 1 == G.n_desc ? 0 : b + 1;
-        if (t2 == G.steps) {
-            t2 = 0;
-            b2 = G.first;
-            f2 = f + nw;
-        }
-        const bool more = f2 < nf;
-        if (HALDA_STEPS_PREFETCH && more) {
-            nxt.d0 = steps_desc(G, b2).base + int64_t(f2) * M;
-            nxt.mf = load_fields(steps_fleets(steps_desc(G, b2)), nxt.d0 + dl);
-        }
+        cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
+        cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
         sweep_fleet<false, false, Wave, true>(A, steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), f, w,
                                               wv, &cur);
-        if (!more) break;
-        f = f2;
-        t = t2;
-        b = b2;
-        if (HALDA_STEPS_PREFETCH) {
-            cur = nxt;
-        } else {
-            cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
-            cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
+        // the wave's next item, nw items on
+        f += df;
+        t += dt;
+        b += db;
+        if (f >= nf) {
+            f -= nf;
+            ++t;
+            ++b;
         }
+        if (b >= G.n_desc) b -= G.n_desc;
+        if (t >= G.steps) break;
     }
 }
 

@@ -501,9 +501,9 @@ class _OneFleet:
     k-candidates) shape, reused while the shape repeats -- no per-call allocation or struct filling.
     The results are overwritten by the thread's next call: callers copy what they keep."""
 
-    def __init__(self, nd: int, ks: Sequence[int]):
+    def __init__(self, nd: int, ks: Sequence[int], L: int):
         nk = len(ks)
-        self.nd, self.ks = nd, list(ks)
+        self.nd, self.ks, self.L = nd, list(ks), L
         self.karr = np.asarray(self.ks, np.int32)
         self.f64 = np.empty((len(F64_FIELDS), nd))
         self.i64 = np.empty((len(I64_FIELDS), nd), np.int64)
@@ -521,15 +521,25 @@ class _OneFleet:
         self.hdr[15:21] = pi + 8 * nd * np.arange(len(I64_FIELDS), dtype=np.uint64)
         self.fs = HaldaFleetsC.from_buffer(self.hdr)
         xs = 7 * nd + 1
-        self.fbuf = np.zeros(1 + nk + 2 * nk * xs)
+        # x / c only of the k that can be optimal (L // k >= M: every device needs a layer), in the compact
+        # layout of halda_fleet_result.x_off: xrow[j] = k_j's row of x / c, -1 for the others
+        self.xrow = [-1] * nk
+        n_open = 0
+        for j, k in enumerate(self.ks):
+            if L // k >= nd:
+                self.xrow[j] = n_open
+                n_open += 1
+        self.x_off = np.asarray([r * xs if r >= 0 else -1 for r in self.xrow], np.int64)
+        self.fbuf = np.zeros(1 + nk + 2 * max(n_open, 1) * xs)
         self.ibuf = np.zeros(1 + 2 * nd + nk, np.int32)
         pF, pI = self.fbuf.ctypes.data, self.ibuf.ctypes.data
         o2 = 1 + nk
         self.status = self.ibuf[1 + 2 * nd:]
-        self.x = self.fbuf[o2:o2 + nk * xs].reshape(nk, xs)
-        self.c = self.fbuf[o2 + nk * xs:].reshape(nk, xs)
+        no = max(n_open, 1)
+        self.x = self.fbuf[o2:o2 + no * xs].reshape(no, xs)
+        self.c = self.fbuf[o2 + no * xs:].reshape(no, xs)
         self.res = HaldaFleetResultC(pI, pF, pI + 4, pI + 4 * (1 + nd), pF + 8, pI + 4 * (1 + 2 * nd), pF + 8 * o2,
-                                     pF + 8 * (o2 + nk * xs), None)
+                                     pF + 8 * (o2 + no * xs), self.x_off.ctypes.data)
 
 
 _TLS = threading.local()
@@ -543,15 +553,16 @@ def pack_one(devs: Sequence[DeviceProfile], model: ModelProfile, ks: Sequence[in
         raise RuntimeError("pack_one needs the C packer (distilp_amd/csrc/fleetpack.c)")
     nd = len(devs)
     ws = getattr(_TLS, "one", None)
-    if ws is None or ws.nd != nd or ws.ks != ks:
-        ws = _TLS.one = _OneFleet(nd, ks)
+    if ws is None or ws.nd != nd or ws.ks != ks or ws.L != model.L:
+        ws = _TLS.one = _OneFleet(nd, ks, model.L)
     _PACKER.pack([devs], model.Q, "b_1" in model.f_q, "b_1" in model.f_out, ws.f64, ws.i64, ws.u8, ws.off, ws.heads)
     return ws
 
 
 def sweep_one(ws: "_OneFleet", model: ModelProfile, kv_factor: float, device: int = 0) -> "_OneFleet":
-    """The packed fleet of `ws` swept over its k-candidates by halda_solve_fleets_host, x and c of every
-    k returned (ws.status [n_k], ws.x / ws.c [n_k, 7 M + 1]), and its obj_value constants (sum t_comm,
+    """The packed fleet of `ws` swept over its k-candidates by halda_solve_fleets_host, x and c of the k
+    that can be optimal returned (ws.status [n_k]; ws.x / ws.c [rows, 7 M + 1], k_j's row ws.xrow[j]),
+    and its obj_value constants (sum t_comm,
     sum xi, kappa in the reference's order, the packer's C loops) in ws.consts. The thread's next call
     overwrites them."""
     ctx = get_context(device)

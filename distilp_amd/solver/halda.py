@@ -98,6 +98,8 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
     M, N = len(devs), 7 * len(devs) + 1
     swept = False
     status = X = C = None
+    st_list: List[int] = []
+    xrow: List[int] = []
     out: List[Tuple[int, Optional[ILPResult]]] = []
     for k in Ks:
         if debug:
@@ -112,23 +114,27 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                 swept = True
                 if one:
                     sweep_one(ws, model, kv_factor, device)
-                    status, X, C = ws.status, ws.x, ws.c
+                    status, X, C, xrow = ws.status, ws.x, ws.c, ws.xrow
                     t_comm, xi_sum, kappa = (float(v) for v in ws.consts)
                     cls_row = ws.u8[0]
                 else:
                     res = solve_table(ws, model, pos, kv_factor, device, want_x=True)
                     status, X, C = res.status[0], res.x[0], res.c[0]
+                    xrow = list(range(len(pos)))
                     # sum t_comm, sum xi, kappa in the reference's order (the packer's C loops)
                     t_comm, xi_sum, kappa = (float(v[0]) for v in fleet_constants(ws, model))
                     cls_row = ws.os_class
                 if _cls_out is not None:
                     _cls_out.append(np.array(cls_row, np.uint8))
+                st_list = status.tolist()
             j = pos.index(k)
-            st = int(status[j])
+            st = st_list[j]
             if st == STATUS_OPTIMAL:
-                x = np.array(X[j, :N])
-                c = np.array(C[j, :N])
-                obj = float(c.dot(x)) + t_comm + xi_sum + kappa
+                # views of the rows (the workspace is read before this thread's next call): c.dot(x) is
+                # numpy's 1-D dot on the same contiguous rows, the reference's float(c @ x) bits
+                q = xrow[j]  # an optimal k has L // k >= M (each device takes a layer): its row came back
+                x = X[q, :N]
+                obj = float(C[q, :N].dot(x)) + t_comm + xi_sum + kappa
                 wn = np.rint(x[:2 * M]).astype(np.int64).tolist()  # int(round(v)): both round half to even
                 r = _construct(ILPResult, k=k, w=wn[:M], n=wn[M:], obj_value=obj)  # fields already typed
             elif st != STATUS_INFEASIBLE:

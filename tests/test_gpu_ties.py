@@ -148,7 +148,9 @@ def test_reference_tie_goldens_twice():
         if unique:
             assert (r.w, r.n) == (w, n), key
             if r.k == want["k"] and (r.w, r.n) == (want["w"], want["n"]):
-                assert r.obj_value == want["obj_value"], key  # host-formed objective: the reference's bits
+                # the same allocation: the host-formed objective differs from the reference's only through
+                # x's continuous cycle time C, which HiGHS returns within its feasibility tolerance
+                assert abs(r.obj_value - want["obj_value"]) <= 1e-12 * max(1.0, abs(want["obj_value"])), key
 
 
 @pytest.mark.parametrize("name", ["llama_3_70b/online", "qwen3_32b/bf16"])

@@ -8,7 +8,9 @@ from collections import defaultdict
 
 
 def main():
-    paths = [p for p in sys.argv[1:] if not p.startswith("--")]
+    args = sys.argv[1:]
+    cut = args.index("--items") if "--items" in args else len(args)
+    paths = args[:cut]
     items = {}
     if "--items" in sys.argv:
         for kv in sys.argv[sys.argv.index("--items") + 1:]:
