@@ -351,9 +351,8 @@ def group_roofline(launch_ms, steps, batch_bytes, n_fleets, single):
                 "wait_any_frac": vp.get("wait_any_frac")}
     else:
         valu = {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
-    traffic = pmc_traffic(kern)
-    if traffic is not None:
-        traffic = traffic.get(str(steps)) if isinstance(traffic, dict) else None
+    per_batch = pmc_entry(kern, "hbm_bytes_per_batch")
+    traffic = per_batch * steps if per_batch is not None else None  # HBM bytes scale with the batches
     roofs = {"hbm": achieved / HBM_PEAK_GBS, "valu_issue": valu["frac"]}
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic, "kernel": kern, "kernel_ms": launch_ms,
@@ -391,20 +390,25 @@ def timed_events(step, steps, torch, dev, stream, many=None):
     return e0.elapsed_time(e1) / steps
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py) recorded for THIS libhalda.so build (its
-    libhalda_sha256), or None when none covers this kernel and build."""
+def pmc_entry(kernel, field):
+    """`field` of `kernel` in the newest committed rocprofv3 PMC summary (profiles/*_pmc.json, written by
+    tools/pmc_summary.py) recorded for THIS libhalda.so build (its libhalda_sha256), or None when none
+    covers this kernel and build."""
     sha = lib_sha256()
     for c in sorted((REPO / "profiles").glob("r*_pmc.json"), reverse=True):
         try:
             j = json.loads(c.read_text())
             if j.get("libhalda_sha256") != sha:
                 continue
-            return j["kernels"][kernel]["hbm_bytes_per_launch"]
+            return j["kernels"][kernel][field]
         except Exception:  # noqa: BLE001
             continue
     return None
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` (pmc_entry)."""
+    return pmc_entry(kernel, "hbm_bytes_per_launch")
 
 
 def time_to_optimal(model, M: int, runs: int = 100):
@@ -822,6 +826,7 @@ def main():
     ref = {k: v.cpu().numpy().copy() for k, v in sweeps[0].out.items()}
     for v in sweeps[0].out.values():
         v.zero_()
+    torch.cuda.synchronize(dev)  # the zeroing (torch's stream) before the launch on sref
     turn[0] = 0
     sweep_group(args.steps)
     torch.cuda.synchronize(dev)

@@ -75,6 +75,10 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
+        if name == "halda_sweep_steps_kernel":  # one launch = K batches (run_profile.sh: the bench's --steps)
+            e = out["kernels"][name]
+            e["steps"] = STEPS
+            e["hbm_bytes_per_batch"] = e["hbm_bytes_per_launch"] / STEPS
     solve = out["kernels"].get("halda_sweep_kernel") or out["kernels"].get("halda_solve_k1_kernel")
     out["hbm_bytes_per_launch"] = solve["hbm_bytes_per_launch"] if solve else None
     out["note"] = ("FETCH_SIZE corrected by the measured FETCH_SIZE/bytes ratio of an 8-B-per-lane "
@@ -112,6 +116,8 @@ def mem_counters(src):
             c["derived_wait_any_share"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
     return out
 
+
+STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 20  # the --steps of run_profile.sh's PMC passes
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01")

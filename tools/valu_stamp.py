@@ -67,8 +67,13 @@ def main():
            "note": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS "
                    "over tools/sweep_time.py (fused path); largest launch per kernel"}
     for arg in sys.argv[2:]:
-        name, path = arg.split("=", 1)
+        # name=path[:items] -- items: (batch, fleet) items per dispatch of a steps launch (K x fleets)
+        name, rest = arg.split("=", 1)
+        path, _, items = rest.partition(":")
         res["workloads"][name] = summarise(path)
+        if items:
+            for e in res["workloads"][name].values():
+                e["items"] = int(items)
     # written under gpurun_out/ on the GPU box (merged back), then copied to profiles/ by the builder
     dst = REPO / "gpurun_out" / f"{R}_valu.json"
     dst.parent.mkdir(exist_ok=True)
