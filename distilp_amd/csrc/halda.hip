@@ -17,6 +17,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -67,6 +69,16 @@ struct Ctx {
     int launch_id = 0;
     void *scratch = nullptr;  // host-API staging (device)
     void *pinned = nullptr;   // host-API staging (pinned host), one PCIe copy each way
+    void *pinned_dev = nullptr;  // its device address (zero-copy small calls), looked up once
+    // the resident single-fleet solver (halda_resident_kernel): its mailbox (fine-grained pinned memory),
+    // stream, exit event, the last request number, whether a launch of it may still be running
+    ResidentBox *rbox = nullptr;
+    void *rbox_dev = nullptr;
+    hipStream_t rstream = nullptr;
+    hipEvent_t rdone = nullptr;
+    uint32_t rseq = 0;
+    bool rlive = false;
+    bool resident = true;  // HALDA_RESIDENT=0 at halda_init: every small call launches its own kernel
     size_t pinned_bytes = 0;
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
@@ -659,12 +671,109 @@ int run_sweep(Ctx *c, SweepPlan &p, hipStream_t s) {
     return HALDA_OK;
 }
 
+// The last call's arguments and plan: a caller repeating a call on the same buffers (a single
+// halda_solve's staging, a re-profiled stream) is not re-planned.
+struct SweepKey {
+    halda_model model;
+    halda_fleets F;
+    halda_fleet_result out;
+    int32_t ks[64];
+    int n_k, path_gen;
+    bool x_zero;
+};
+
+int cached_plan(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
+                const halda_fleet_result &out, SweepPlan **plan) {
+    static thread_local SweepKey last_key;
+    static thread_local SweepPlan last_plan;
+    static thread_local const Ctx *last_ctx = nullptr;
+    SweepKey k;
+    std::memset(&k, 0, sizeof k);
+    k.model = model;
+    k.F = F;
+    k.out = out;
+    std::memcpy(k.ks, kh, sizeof(int32_t) * size_t(n_k));
+    k.n_k = n_k;
+    k.path_gen = c->path_gen;
+    k.x_zero = c->x_zero;
+    if (last_ctx != c || std::memcmp(&k, &last_key, sizeof k) != 0) {
+        last_ctx = nullptr;
+        const int rc = plan_sweep(c, model, F, kh, n_k, out, &last_plan);
+        if (rc != HALDA_OK) return rc;
+        last_key = k;
+        last_ctx = c;
+    }
+    *plan = &last_plan;
+    return HALDA_OK;
+}
+
 int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const int32_t *kh, int n_k,
                  const halda_fleet_result &out, hipStream_t s) {
-    SweepPlan p;
-    const int rc = plan_sweep(c, model, F, kh, n_k, out, &p);
+    SweepPlan *p = nullptr;
+    const int rc = cached_plan(c, model, F, kh, n_k, out, &p);
     if (rc != HALDA_OK) return rc;
-    return run_sweep(c, p, s);
+    return run_sweep(c, *p, s);
+}
+
+// One fleet through the resident wave (halda_resident_kernel), synchronously: the plan's arguments into
+// the mailbox, the wave (re)launched when no launch of it is running, seq bumped, ack awaited. The
+// fleet's table and results are the caller's fine-grained pinned buffers (device addresses in A).
+// *done = false when the plan is not a register-only sweep of one fleet (the caller launches it).
+constexpr uint32_t kResidentIdleTicks = 200000;  // 2 ms of the 100 MHz clock without a request
+
+int resident_sweep(Ctx *c, const SweepPlan &p, bool *done) {
+    *done = false;
+    if (!c->resident || p.kind != kRegAlone || p.nf != 1 || p.A.uM <= 0 || p.A.uM > kK1MaxM || p.A.k1dp) return HALDA_OK;
+    if (!c->rbox) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->rbox), sizeof(ResidentBox),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(static_cast<void *>(c->rbox), 0, sizeof(ResidentBox));
+        HIP_TRY(hipHostGetDevicePointer(&c->rbox_dev, c->rbox, 0));
+        HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->rdone, hipEventDisableTiming));
+        c->rseq = 0;
+    }
+    ResidentBox *box = c->rbox;
+    SweepArgs A = p.A;
+    A.fflag = nullptr;
+    A.hb_flag = c->hb_flag;
+    A.launch_id = ++c->launch_id;
+    A.want = 0;
+    std::memcpy(static_cast<void *>(&box->req), &A, sizeof A);
+    auto launch = [&](uint32_t last) -> int {
+        ResidentArgs R;
+        R.box = static_cast<ResidentBox *>(c->rbox_dev);
+        R.last = last;
+        R.idle_ticks = kResidentIdleTicks;
+        hipLaunchKernelGGL(halda_resident_kernel, dim3(1), dim3(64), 0, c->rstream, R);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->rdone, c->rstream));
+        c->rlive = true;
+        return HALDA_OK;
+    };
+    if (!c->rlive || hipEventQuery(c->rdone) == hipSuccess) {
+        const int rc = launch(c->rseq);
+        if (rc != HALDA_OK) return rc;
+    }
+    const uint32_t want = ++c->rseq;
+    __atomic_store_n(&box->seq, want, __ATOMIC_SEQ_CST);  // after the request (x86: stores in order)
+    // the answer; a wave that left (idle timeout) between its last poll and this request is relaunched
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        if (__atomic_load_n(&box->ack, __ATOMIC_ACQUIRE) == want) break;
+        if ((spin & 255) == 0) {
+            if (hipEventQuery(c->rdone) == hipSuccess && __atomic_load_n(&box->ack, __ATOMIC_ACQUIRE) != want) {
+                const int rc = launch(want - 1);
+                if (rc != HALDA_OK) return rc;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                c->resident = false;  // never again on this context: back to a launch per call
+                return fail(HALDA_E_HIP, "resident solver: no answer within 5 s");
+            }
+        }
+    }
+    *done = true;
+    return HALDA_OK;
 }
 
 // ---------------------------------------------------------------- latency mode over RCCL
@@ -902,6 +1011,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->seg_sweep = !(fp && std::strcmp(fp, "wave") == 0);
     const char *hp = std::getenv("HALDA_HOST_PATH");  // diagnostic A/B of the small synchronous call
     c->host_copy = hp && std::strcmp(hp, "copy") == 0;
+    const char *rs = std::getenv("HALDA_RESIDENT");
+    c->resident = !(rs && std::strcmp(rs, "0") == 0);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
@@ -921,6 +1032,15 @@ void halda_free(void *ctx) {
     if (!c) return;
     for (CtxHandle *h : c->handles) h->c = nullptr;  // plans / groups outliving the context fail cleanly
     c->handles.clear();
+    if (c->rbox) {
+        if (c->rlive) {  // the resident wave leaves at its next poll
+            __atomic_store_n(&c->rbox->stop, 1u, __ATOMIC_SEQ_CST);
+            (void)hipEventSynchronize(c->rdone);
+        }
+        (void)hipHostFree(c->rbox);
+    }
+    if (c->rdone) (void)hipEventDestroy(c->rdone);
+    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     (void)hipSetDevice(c->device);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -1129,7 +1249,8 @@ int halda_solve_fleets(void *ctx, const halda_model *model, const halda_fleets *
         const int rc = check_fleets_args(model, fleets, ks, n_k, out);
         if (rc != HALDA_OK) return rc;
     }
-    HIP_TRY(hipSetDevice(c->device));
+    int cur_dev = -1;
+    if (hipGetDevice(&cur_dev) != hipSuccess || cur_dev != c->device) HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     const int32_t *kh = ks;
     // the fused sweep orders itself: per-stream scratch slots, and order_after_previous before a launch
@@ -1496,8 +1617,11 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     if (off > c->pinned_bytes) {
         if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
         c->pinned = nullptr;
+        c->pinned_dev = nullptr;
         c->pinned_bytes = 0;
-        HIP_TRY(hipHostMalloc(&c->pinned, off, hipHostMallocDefault));
+        // fine-grained (coherent): the resident wave reads and writes it between host accesses without a
+        // kernel boundary in between
+        HIP_TRY(hipHostMalloc(&c->pinned, off, hipHostMallocMapped | hipHostMallocCoherent));
         c->pinned_bytes = off;
     }
     char *pin = static_cast<char *>(c->pinned);
@@ -1526,9 +1650,8 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     if (xsel) HIP_TRY(up(o_xoff, out_h->x_off, 8 * size_t(nf) * n_k));
     const bool zc = off <= kZeroCopyBytes && !c->host_copy;
     if (zc) {
-        void *dp = nullptr;
-        HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
-        base = static_cast<char *>(dp);
+        if (!c->pinned_dev) HIP_TRY(hipHostGetDevicePointer(&c->pinned_dev, c->pinned, 0));
+        base = static_cast<char *>(c->pinned_dev);
     } else {
         HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));  // the table (and x_off)
     }
@@ -1555,10 +1678,28 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     // (stores across PCIe, most of a one-fleet k-sweep's time); the copy-out below zero-fills them
     const bool host_zero = zc && c->fleets_fused && (r.x || r.c) && !xsel;
     c->x_zero = !host_zero;
-    const int rc = halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
+    bool resident = false;
+    if (zc && nf == 1 && c->fleets_fused && c->resident && n_k <= 64) {
+        // one fleet, the register-only plan: the resident wave, no launch
+        const int rc0 = check_fleets_args(model, &d, ks, n_k, &r);
+        if (rc0 != HALDA_OK) {
+            c->x_zero = true;
+            return rc0;
+        }
+        SweepPlan *p = nullptr;
+        int rc1 = cached_plan(c, *model, d, ks, n_k, r, &p);
+        if (rc1 == HALDA_OK) rc1 = resident_sweep(c, *p, &resident);
+        if (rc1 != HALDA_OK) {
+            c->x_zero = true;
+            return rc1;
+        }
+    }
+    const int rc = resident ? HALDA_OK : halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
     c->x_zero = true;
     if (rc != HALDA_OK) return rc;
-    if (zc) {
+    if (resident) {
+        // the results are in the pinned buffer (ack was published after them)
+    } else if (zc) {
         HIP_TRY(hipEventRecord(c->ev_host, s));
         hipError_t q;
         while ((q = hipEventQuery(c->ev_host)) == hipErrorNotReady) {

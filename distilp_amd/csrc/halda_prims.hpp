@@ -54,10 +54,6 @@ __device__ unsigned long long g_halda_scanprof[kStampInst * kScanProf];
         if (q < SA.n_slot && (threadIdx.x & 63) == 0 && e_ < kStampInst)                                \
             g_halda_stamps[e_ * kStamps + (slot)] = (v);                                                \
     } while (0)
-#elif defined(HALDA_MARKS)  // asm listing only: phase markers for tools/asm_regions.py
-#define HALDA_SSTAMP(slot, v) asm volatile("; PHASE_MARK " #slot)
-#define HALDA_TSTAMP(slot) do {} while (0)
-#define HALDA_STAMP(k) do {} while (0)
 #else
 #define HALDA_SSTAMP(slot, v) \
     do {                      \

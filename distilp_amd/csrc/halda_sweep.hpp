@@ -721,7 +721,7 @@ __device__ inline double kappa_head(const halda_model &Mo, int flags, double scp
     return total;
 }
 
-template <class SG>
+template <class SG, bool kLds = false>
 __device__ inline void fleet_offsets_regs(const SweepModel &Mo, const DevFields &mf, int M, const SG &sg, double &tsum,
                                           double &xsum, double &kappa) {
     const bool act = sg.sl < M;
@@ -741,7 +741,11 @@ __device__ inline void fleet_offsets_regs(const SweepModel &Mo, const DevFields 
     // the four numerators as register values: a select chain over kernel arguments is otherwise turned
     // into a per-lane vector load from the argument segment (a vector memory wait of its own)
     double n0 = Mo.f_out_b1, n1 = Mo.bvo, n2 = Mo.b_in, n3 = Mo.b_out;
-    asm volatile("" : "+s"(n0), "+s"(n1), "+s"(n2), "+s"(n3));
+    if constexpr (kLds) {  // the model read from LDS: vector registers
+        asm volatile("" : "+v"(n0), "+v"(n1), "+v"(n2), "+v"(n3));
+    } else {
+        asm volatile("" : "+s"(n0), "+s"(n1), "+s"(n2), "+s"(n3));
+    }
     const double num = j == 0 ? n0 : j == 1 ? n1 : j == 2 ? n2 : n3;
     const double den = j == 0 ? scpu : j == 1 ? Tc : j == 2 ? Mo.V * sdisk : sdisk;
     const double q = num / den;
@@ -883,8 +887,10 @@ struct SweepPre {
 };
 
 // F / O: the batch's table and results (the kernel arguments' A.F / A.out, or one batch of a steps
-// launch); kPre: the fleet's fields come prefetched in *pre (every fleet has A.uM <= kK1MaxM devices).
-template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false>
+// launch); kPre: the fleet's fields come prefetched in *pre (every fleet has A.uM <= kK1MaxM devices);
+// kXC = false: the x / c outputs are compiled out (the caller guarantees outs has none); kLds: A is in
+// LDS (the resident wave), its uniform fields arrive in vector registers.
+template <bool kTables, bool kGlobal, class SG = Wave, bool kPre = false, bool kXC = !kPre, bool kLds = false>
 __device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const FleetOut &O, int f, const WaveCtx &w,
                             const SG &sg, const SweepPre *pre = nullptr) {
     constexpr int S = SG::S;
@@ -906,7 +912,7 @@ __device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const Fle
     int64_t d0 = kPre ? pre->d0 : A.uM > 0 ? int64_t(f) * A.uM : F.dev_off[f];
     const int M = kPre ? A.uM : A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - d0);
     // the outputs this call writes (a steps launch has no x / c: those paths compile out of it)
-    const int outs = kPre ? A.outs & (kOutObk | kOutSt) : A.outs;
+    const int outs = kXC ? A.outs : A.outs & (kOutObk | kOutSt);
     bool regs = M <= kK1MaxM;  // lane = device: the k = 1 greedy runs in registers
     if constexpr (kSeg || kPre) regs = true;  // the host sends fleets of at most S / kK1MaxM devices
     FieldRec me = {};
@@ -930,7 +936,7 @@ __device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const Fle
         }
         me = field_rec(Mo, mf, bad);
         bad = lane < M ? bad : 0;
-        if (M > 0) fleet_offsets_regs(Mo, mf, M, sg, tsum, xsum, kappa);
+        if (M > 0) fleet_offsets_regs<SG, kLds>(Mo, mf, M, sg, tsum, xsum, kappa);
     } else {
         if (A.uM > 0) d0 += sload_i64(F.dev_off);
         for (int i = lane; i < M; i += 64) {
@@ -990,7 +996,7 @@ __device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const Fle
         // fleets open one k)
         opaque_rec(me);
         int M = M_all;
-        if constexpr (!kSeg) asm volatile("" : "+s"(M));
+        if constexpr (!kSeg && !kLds) asm volatile("" : "+s"(M));
         const int k = sg.bcast(kj, j);
         const int W = sg.bcast(Wj, j);
         const int64_t inst = int64_t(f) * A.n_k + j;
@@ -1379,6 +1385,79 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void h
         }
         if (b >= G.n_desc) b -= G.n_desc;
         if (t >= G.steps) break;
+    }
+}
+
+// ---------------------------------------------------------------- resident single-fleet solver
+// halda_resident_kernel: ONE wave that stays resident between single-fleet calls (halda_solve's
+// latency path through halda_solve_fleets_host): the host writes the call's sweep arguments and the
+// fleet's table into fine-grained pinned memory and bumps `seq`; the wave, polling `seq` across PCIe,
+// copies the arguments into LDS, solves the fleet exactly as the per-call register launch does (the
+// same sweep_fleet on the same fields, x / c included) writing into the pinned results, and publishes
+// `ack` = seq with a system-scope release. No launch and no completion event per call. It leaves when
+// the host sets `stop` or after `idle_ticks` of the 100 MHz real-time clock without a request (every
+// wave exits: the host relaunches it on its next call), so it never outlives its process by more
+// than that. All its stores are vector stores.
+struct ResidentBox {
+    uint32_t seq;  // host: request number, written after the request
+    uint32_t pad0[15];
+    uint32_t ack;  // device: the last request done
+    uint32_t pad1[15];
+    uint32_t stop;  // host: 1 = leave now
+    uint32_t pad2[15];
+    SweepArgs req;  // host: the request's sweep arguments (one fleet, a register-only plan)
+};
+
+struct ResidentArgs {
+    ResidentBox *box;
+    uint32_t last;        // the request number already answered
+    uint32_t idle_ticks;  // s_memrealtime ticks (100 MHz) without a request before the wave leaves
+};
+
+__device__ inline uint32_t sys_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void halda_resident_kernel(ResidentArgs R) {
+    __shared__ SweepArgs As;
+    __shared__ uint8_t dparg[64 * kDpLanes];
+    const int lane = int(threadIdx.x);
+    WaveCtx w = {};
+    w.dparg = dparg;
+    const Wave wv(lane);
+    uint32_t last = R.last;
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+        const uint32_t stop = sys_load(&R.box->stop);
+        const uint32_t seq = sys_load(&R.box->seq);
+        if (stop) break;
+        if (seq == last) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request and table written before seq
+        // the sweep arguments into LDS by vector loads (nothing of the request is read through the
+        // scalar cache, which does not see the host's writes)
+        constexpr int kWords = int(sizeof(SweepArgs) / 4);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(&R.box->req);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(&As);
+        for (int i = lane; i < kWords; i += 64) dst[i] = sys_load(src + i);
+        __builtin_amdgcn_s_waitcnt(0);
+        wave_sync();
+        SweepPre pre;
+        const bool kl = lane < As.n_k;
+        pre.kj = As.ks[kl ? lane : 0];
+        pre.Wj = kl ? As.Ws[lane] : 0;
+        pre.d0 = 0;
+        const int M = As.uM;
+        pre.mf = load_fields(As.F, lane < M ? lane : 0);
+        sweep_fleet<false, false, Wave, true, true, true>(As, As.F, As.out, 0, w, wv, &pre);
+        // every result store before ack (system-scope release: the host reads them after it)
+        if (lane == 0) __hip_atomic_store(&R.box->ack, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+        t0 = __builtin_amdgcn_s_memrealtime();
+        wave_sync();
     }
 }
 

@@ -23,6 +23,7 @@ on a missing batch key, IndexError on an empty fleet) surface the same way.
 from __future__ import annotations
 
 import math
+import sys
 from typing import Dict, List, Optional, Tuple
 
 from pydantic import BaseModel
@@ -30,9 +31,17 @@ from pydantic import BaseModel
 from ..common import DeviceProfile, ModelProfile
 
 
+_FACTORS: Dict[int, Tuple[str, List[int]]] = {}
+
+
 def valid_factors_of_L(L: int) -> List[int]:
     """Divisors of L other than L, sorted. Prints the unsorted discovery list
-    exactly like the reference (dense_common.py:21), which the CLI shows."""
+    exactly like the reference (dense_common.py:21), which the CLI shows (the printed line and the
+    list are remembered per integer L: the same text, written in one call)."""
+    hit = _FACTORS.get(L) if type(L) is int else None
+    if hit is not None:
+        sys.stdout.write(hit[0])
+        return list(hit[1])
     found: List[int] = []
     for d in range(1, int(math.sqrt(L)) + 1):
         if L % d:
@@ -43,7 +52,10 @@ def valid_factors_of_L(L: int) -> List[int]:
         if q != d and q != L:
             found.append(q)
     print(L, found)
-    return sorted(set(found))
+    out = sorted(set(found))
+    if type(L) is int:
+        _FACTORS[L] = (f"{L} {found}\n", out)
+    return out
 
 
 def b_prime(model: ModelProfile, kv_bits_k: float = 1.0, kv_bits_v: Optional[float] = None,

@@ -1,4 +1,4 @@
-"""Summarise a profiles/run_profile.sh run into profiles/<round>_*.
+"""Summarise a profiles/run_round.sh run into profiles/<round>_*.
 
 Writes:
   profiles/<R>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
@@ -75,7 +75,7 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-        if name == "halda_sweep_steps_kernel":  # one launch = K batches (run_profile.sh: the bench's --steps)
+        if name == "halda_sweep_steps_kernel":  # one launch = K batches (run_round.sh: the bench's --steps)
             e = out["kernels"][name]
             e["steps"] = STEPS
             e["hbm_bytes_per_batch"] = e["hbm_bytes_per_launch"] / STEPS
@@ -86,38 +86,10 @@ def main(R):
                    "WRITE_SIZE taken as bytes. Largest launch per kernel = the C3 batch.")
     (dst / f"{R}_pmc.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
-    mem = mem_counters(src)
-    if mem:
-        (dst / f"{R}_pmc_mem.json").write_text(json.dumps(mem, indent=1))
 
 
-def mem_counters(src):
-    """profiles/run_pmc_mem.sh passes: per kernel, the counters of its largest (C3) launch."""
-    out = {}
-    for p in ("pmc_ta", "pmc_tcp", "pmc_tcc", "pmc_tlb"):
-        f = src / p / "run_counter_collection.csv"
-        if not f.exists():
-            continue
-        d = defaultdict(lambda: defaultdict(list))
-        for r in csv.DictReader(open(f)):
-            k = short(r["Kernel_Name"])
-            if "halda" in k:
-                d[k][r["Counter_Name"]].append((int(r.get("Grid_Size", 0) or 0), float(r["Counter_Value"])))
-        for k, cs in d.items():
-            for c, v in cs.items():
-                g = max(x[0] for x in v)
-                out.setdefault(k, {})[c] = statistics.median(x[1] for x in v if x[0] == g)
-    for k, c in out.items():
-        if c.get("TCP_TCC_READ_REQ_sum"):
-            c["derived_l1_l2_read_latency_cycles"] = c.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / c["TCP_TCC_READ_REQ_sum"]
-        if c.get("TCC_REQ_sum"):
-            c["derived_l2_hit_rate"] = c.get("TCC_HIT_sum", 0.0) / c["TCC_REQ_sum"]
-        if c.get("SQ_WAVE_CYCLES"):
-            c["derived_wait_any_share"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
-    return out
 
-
-STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 20  # the --steps of run_profile.sh's PMC passes
+STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 20  # the --steps of run_round.sh's PMC passes
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01")

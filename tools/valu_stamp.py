@@ -1,7 +1,7 @@
 """Record the VALU count per wave of the fused-sweep kernels for THIS libhalda.so build.
 
 Run on the GPU box right after the counter passes (same snapshot, so the hashed library is the one
-profiled), e.g. via profiles/run_valu.sh:
+profiled), e.g. via profiles/run_round.sh:
 
   python tools/valu_stamp.py r03 c3=gpurun_out/valu_c3/run_counter_collection.csv \
                                  c2=gpurun_out/valu_c2/run_counter_collection.csv
