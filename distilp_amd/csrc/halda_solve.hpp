@@ -1283,6 +1283,12 @@ __device__ inline void split_publish(SplitArea *ar, int lane, bool act, int lo, 
 
 // Phase 0 of a k > 1 instance: the unconstrained greedy exchange from e = lo (rounds: the smallest next
 // increment wins and keeps every one still beating the runner-up); e ends at the allocation.
+// Every round either takes at least one layer or stops: a row that is not checked yet (the optimistic
+// k-slot part 1's helper runs this before the leaf checks' verdict) may hold an infinite entry inside
+// its finite ends, whose increments are inf or NaN; no finite increment left, or a run of length 0,
+// ends the loop with the allocation incomplete, and that row's failed leaf check (contiguity) sends
+// the fleet to the table launch before anyone uses it. (A FieldRec row cannot have such a gap: its
+// feasible n-interval only shrinks as w grows, so an infeasible w stays infeasible above.)
 template <class SG>
 __device__ inline void phase0_greedy(const double *Gall, int RS, int need, const SG &sg, bool act, int hi, int &e) {
     const int lane = sg.sl;
@@ -1290,11 +1296,13 @@ __device__ inline void phase0_greedy(const double *Gall, int RS, int need, const
     double inc = act && e < hi ? G[e + 1] - G[e] : kInf;
     while (need > 0) {
         const double bv = sg.min_f64(inc);
+        if (!(bv < kInf)) break;  // no device can take a layer (or NaN increments): leave it to the checks
         const int win = sg.lowest(inc == bv);
         const double rv = lane == win ? kInf : inc;
         const double m2 = sg.min_f64(rv);
         const int d2 = sg.lowest(rv == m2);
         const int t = take_run(Gall + int64_t(win) * RS, sg.bcast(e, win), sg.bcast(hi, win), need, m2, win < d2, sg);
+        if (t <= 0) break;
         if (lane == win) {
             e += t;
             inc = e < hi ? G[e + 1] - G[e] : kInf;
