@@ -520,9 +520,10 @@ def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
 def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     """Config C2 (BASELINE.json configs[1]) as its own leg: 4096 synthetic M = 16 fleets x every k of
     L = 80 (k = 1, 2, 4, 5 feasible: the k > 1 MILPs of halda_p_solver.py:391-412 are solved here), one
-    halda_solve_fleets k-sweep per step from resident tables; its own roofline from the one-stream launch
-    time of its dominant kernel."""
-    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation, fleet_table
+    k-sweep per step from resident tables: the K steps as ONE group launch (the k-slot form:
+    halda_sweep_kslot_steps_kernel + the gated table launch), beside it as K launches over two streams and
+    over one stream; its own roofline from the per-batch k-slot launch time."""
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup, PlanRotation, fleet_table
 
     M2 = 16
     table = fleet_table(build_fleets(range(C3_FLEETS), M2), model)
@@ -568,7 +569,18 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     bk = tabs[(turn[0] - 1) % n].out["best_k"].cpu().numpy()
     if not (bk > 0).all():
         raise RuntimeError("C2: a fleet without a feasible k")
-    steps = max(10, args.steps // 4)
+    steps = args.steps
+    alg = sweep_bytes(table)
+    group = PlanGroup(tabs, ctx)
+
+    def manyg(k):
+        group.launch(turn[0], k, stream.cuda_stream)
+        turn[0] += k
+
+    manyg(steps)  # warm
+    torch.cuda.synchronize(dev)
+    elg = timed(None, steps, torch, dev, None, 1, many=manyg)
+    evg = statistics.median(timed_events(None, 1, torch, dev, stream, many=lambda _: manyg(steps)) for _ in range(3))
     el2 = timed(step2, steps, torch, dev, None, 1, many=many2)
     ev1 = timed_events(step1, steps, torch, dev, stream, many=many1)
     ctx.set_timing(True)
@@ -579,12 +591,16 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
         per.append(ctx.last_fleet_ms())
     ctx.set_timing(False)
     ph = {k: statistics.mean(p.get(k, 0.0) for p in per) for k in per[0]}
-    alg = sweep_bytes(table)
     inst = C3_FLEETS * len(KS_L80)
     return {
         "workload": f"C2: {C3_FLEETS} synthetic M={M2} fleets x {len(KS_L80)} k-candidates (L=80, llama_3_70b/online, "
                     "kv 4bit) per step, one halda_solve_fleets k-sweep from resident tables",
         "instances_per_step": inst, "feasible_per_step": n_opt,
+        "ms_per_step": elg / steps * 1e3, "instances_per_s": inst * steps / elg,
+        "group_launch": {"persistent": group.persistent, "launch_ms": evg, "ms_per_batch_events": evg / steps,
+                         "alg_GBps": alg * steps / (evg * 1e-3) / 1e9,
+                         "what": "the K steps as one group launch (k-slot steps kernel + the gated table launch), "
+                                 "HIP events around it on its stream, median of 3"},
         "ms_per_step_one_stream": ev1, "instances_per_s_one_stream": inst / (ev1 * 1e-3),
         "ms_per_step_two_streams": el2 / steps * 1e3, "instances_per_s_two_streams": inst * steps / el2,
         "steps": steps, "resident_copies": n,

@@ -1432,10 +1432,15 @@ void halda_fleets_plan_free(void *plan) {
 namespace {
 struct FleetsGroup : CtxHandle {
     std::vector<FleetsPlan> plans;  // copies: the group does not depend on the caller's plan handles
-    bool persistent = false;        // every plan a register sweep of one shape: the steps kernel applies
+    bool persistent = false;        // every plan a register (or k-slot) sweep of one shape: one launch
+    bool kslot = false;             // ... the k-slot form (halda_sweep_kslot_steps_kernel + gated tables)
     int gen = 0;                    // the context's path_gen when the group was checked
     SweepArgs A;                    // the first plan's arguments (shape, model, k list)
     StepsDesc *desc = nullptr;      // device copy of the plans' tables / results
+    uint8_t *fflag = nullptr;       // k-slot form: per (plan, fleet) hand-back flags
+    int *hb = nullptr;              // ... the launch's hand-back flag
+    unsigned *ctr = nullptr;        // ... the launch's item counter
+    int64_t lds = 0;                // ... the k-slot launch's LDS (the plan's + the next-item slot)
     unsigned grid = 0;
 };
 
@@ -1453,11 +1458,15 @@ int group_check(FleetsGroup *G) {
         }
     }
     const FleetsPlan &P0 = G->plans[0];
-    bool ok = P0.fused && P0.p.kind == kRegAlone && P0.p.A.uM > 0 && P0.p.A.uM <= kK1MaxM &&
-              !(P0.p.A.outs & kOutXC) && !P0.p.A.x_off && !P0.p.A.k1dp;
+    const bool reg = P0.fused && P0.p.kind == kRegAlone && P0.p.A.uM > 0 && P0.p.A.uM <= kK1MaxM && !P0.p.A.k1dp;
+    const bool ksl = P0.fused && P0.p.kind == kKslotGated;
+    bool ok = (reg || ksl) && !(P0.p.A.outs & kOutXC) && !P0.p.A.x_off;
     for (const FleetsPlan &P : G->plans) {
-        ok = ok && P.fused && P.p.kind == kRegAlone && P.F.n_fleets == P0.F.n_fleets && P.p.A.uM == P0.p.A.uM &&
-             P.p.A.outs == P0.p.A.outs && P.ks == P0.ks && same_model(P.model, P0.model) && !P.p.A.x_off;
+        ok = ok && P.fused && P.p.kind == P0.p.kind && P.F.n_fleets == P0.F.n_fleets && P.p.A.uM == P0.p.A.uM &&
+             P.F.min_devices == P0.F.min_devices && P.F.max_devices == P0.F.max_devices &&
+             P.p.A.outs == P0.p.A.outs && P.ks == P0.ks && same_model(P.model, P0.model) && !P.p.A.x_off &&
+             P.p.lds == P0.p.lds && P.p.slice == P0.p.slice && P.p.grid2 == P0.p.grid2 &&
+             P.p.block1 == P0.p.block1 && std::memcmp(&P.p.SA, &P0.p.SA, sizeof(SlotArgs)) == 0;
     }
     if (!ok) return HALDA_OK;
     std::vector<StepsDesc> h(G->plans.size());
@@ -1472,11 +1481,26 @@ int group_check(FleetsGroup *G) {
     if (!G->desc) HIP_TRY(hipMalloc(&G->desc, sizeof(StepsDesc) * h.size()));
     HIP_TRY(hipMemcpy(G->desc, h.data(), sizeof(StepsDesc) * h.size(), hipMemcpyHostToDevice));
     G->A = P0.p.A;
-    // every wave resident at once: the occupancy of the steps kernel on every CU (the launch caps it at
-    // one wave per item)
+    G->kslot = ksl;
+    // every workgroup resident at once: the occupancy of the steps kernel on every CU (the launch caps it
+    // at one workgroup per item)
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(halda_sweep_steps_kernel),
-                                                         64 * kSweepWavesPerBlock, 0));
+    if (ksl) {
+        const void *fn = reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel);
+        G->lds = align16(P0.p.lds) + 16;
+        HIP_TRY(Ctx::ensure_lds(fn, G->lds));
+        HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_tables_steps_kernel), P0.p.slice));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, int(P0.p.block1), size_t(G->lds)));
+        if (!G->ctr) HIP_TRY(hipMalloc(&G->ctr, 256));
+        const size_t nfl = h.size() * size_t(P0.F.n_fleets);
+        if (!G->fflag) HIP_TRY(hipMalloc(&G->fflag, std::max<size_t>(nfl, 1)));
+        if (!G->hb) HIP_TRY(hipMalloc(&G->hb, sizeof(int)));
+        HIP_TRY(hipMemset(G->fflag, 0, std::max<size_t>(nfl, 1)));
+        HIP_TRY(hipMemset(G->hb, 0, sizeof(int)));
+    } else {
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void *>(halda_sweep_steps_kernel), 64 * kSweepWavesPerBlock, 0));
+    }
     G->grid = unsigned(std::max(per_cu, 1) * c->cus);
     G->persistent = true;
     return HALDA_OK;
@@ -1502,6 +1526,9 @@ int halda_fleets_group_create(void *const *plans, int32_t n_plans, void **group,
     const int rc = group_check(G);
     if (rc != HALDA_OK) {
         if (G->desc) (void)hipFree(G->desc);
+        if (G->fflag) (void)hipFree(G->fflag);
+        if (G->hb) (void)hipFree(G->hb);
+        if (G->ctr) (void)hipFree(G->ctr);
         delete G;
         return rc;
     }
@@ -1540,21 +1567,51 @@ int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *s
     SG.n_desc = int(n);
     SG.first = int(first % n);
     SG.steps = steps;
+    SG.fflag = G->fflag;
+    SG.ctr = nullptr;
+    SG.next_off = 0;
     c->fleet_timed = false;
     c->have_lowered = false;
+    const int nf = G->plans[0].F.n_fleets;
     if (c->timing) HIP_TRY(hipEventRecord(c->evf0, s));
-    const int64_t items = int64_t(steps) * G->plans[0].F.n_fleets;
-    const unsigned grid = unsigned(std::min<int64_t>(G->grid, (items + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock));
-    hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
-    HIP_TRY(hipGetLastError());
+    if (G->kslot) {
+        const SweepPlan &p = G->plans[0].p;
+        SweepArgs A = G->A;
+        A.fflag = nullptr;  // per batch: SG.fflag
+        A.hb_flag = G->hb;
+        A.launch_id = ++c->launch_id;
+        A.want = 0;
+        const int64_t items = int64_t(steps) * ((nf + 64 / kSegLanes - 1) / (64 / kSegLanes));
+        if (items > (int64_t(1) << 31) - 1) return fail(HALDA_E_ARG, "halda_fleets_group_launch: too many items");
+        const unsigned grid = unsigned(std::min<int64_t>(G->grid, items));
+        SG.ctr = G->ctr;
+        SG.next_off = int(G->lds - 16);
+        HIP_TRY(hipMemsetAsync(G->ctr, 0, sizeof(unsigned), s));
+        HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel), G->lds));
+        hipLaunchKernelGGL(halda_sweep_kslot_steps_kernel, dim3(grid), dim3(p.block1), size_t(G->lds), s, A, p.SA,
+                           SG);
+        HIP_TRY(hipGetLastError());
+        if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
+        A.want = 1;  // the fleets flagged above, gated on the launch's hand-back flag
+        HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_tables_steps_kernel), p.slice));
+        hipLaunchKernelGGL(halda_sweep_tables_steps_kernel, dim3(p.grid2, unsigned(std::min<int64_t>(steps, n))),
+                           dim3(64), size_t(p.slice), s, A, SG);
+        HIP_TRY(hipGetLastError());
+    } else {
+        const int64_t items = int64_t(steps) * nf;
+        const unsigned grid =
+            unsigned(std::min<int64_t>(G->grid, (items + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock));
+        hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
+        HIP_TRY(hipGetLastError());
+    }
     if (c->timing) {
         HIP_TRY(hipEventRecord(c->evf1, s));
         c->fleet_timed = true;
     }
-    c->fleet_two = false;
-    c->fleet_reg_alone = true;
+    c->fleet_two = G->kslot;
+    c->fleet_reg_alone = !G->kslot;
     c->fleet_seg = false;
-    c->fleet_kslot = false;
+    c->fleet_kslot = G->kslot;
     c->last_fleet_fused = true;
     return HALDA_OK;
 }
@@ -1567,6 +1624,9 @@ void halda_fleets_group_free(void *group) {
         G->c->detach(G);
     }
     if (G->desc) (void)hipFree(G->desc);
+    if (G->fflag) (void)hipFree(G->fflag);
+    if (G->hb) (void)hipFree(G->hb);
+    if (G->ctr) (void)hipFree(G->ctr);
     delete G;
 }
 

@@ -834,6 +834,18 @@ struct SweepArgs {
     int32_t Ws[64];  // W = L / k per k (host integer division)
 };
 
+// The per-batch part of a sweep's arguments: the table, the results and the per-fleet hand-back flags
+// (a launch's own A.F / A.out / A.fflag, or one batch of a steps launch).
+// References, so that a launch's own view reads the kernel arguments where they are (no copy held in
+// registers).
+struct SweepBatch {
+    const halda_fleets &F;
+    const FleetOut &out;
+    uint8_t *fflag;
+};
+
+__device__ inline SweepBatch batch_of(const SweepArgs &A) { return SweepBatch{A.F, A.out, A.fflag}; }
+
 // Element offset of instance inst's x / c: the dense layout, or the caller's compact x_off (-1: not
 // written).
 __device__ inline int64_t xc_at(const SweepArgs &A, int64_t inst) {
@@ -865,14 +877,15 @@ __device__ inline void put_xc(const SweepArgs &A, const FleetOut &O, int64_t ins
 #define HALDA_SWEEP_TABLE_K1 1  // table launches also run the k = 1 register greedy (else k = 1 via tables)
 #endif
 
-__device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) {
+__device__ inline void flag_fleet(const SweepArgs &A, uint8_t *fflag, int f, int lane) {
     // the scratch-free register launch (fflag == nullptr) never flags: sweep_fleets runs it alone only
     // when nothing in the batch can need the table launch (no k > 1 with W >= M, R + 1 <= kDpLanes)
-    if (lane == 0 && A.fflag) {
-        A.fflag[f] = 1;
+    if (lane == 0 && fflag) {
+        fflag[f] = 1;
         __hip_atomic_store(A.hb_flag, A.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
+__device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) { flag_fleet(A, A.fflag, f, lane); }
 
 // SG = Wave: one fleet per wave; SG = Seg<16>: one fleet (M <= 16, n_k <= 16) per 16-lane segment,
 // tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
@@ -1225,7 +1238,7 @@ __device__ void sweep_fleet(const SweepArgs &A, const halda_fleets &F, const Fle
 }
 
 template <bool kTables, bool kGlobal>
-__device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base) {
+__device__ inline void sweep_body(const SweepArgs &A, const SweepBatch &B, unsigned char *slice_base) {
     const int lane = threadIdx.x;
     if (A.want == 1 && __hip_atomic_load(A.hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.launch_id)
         return;
@@ -1247,14 +1260,14 @@ __device__ inline void sweep_body(const SweepArgs &A, unsigned char *slice_base)
         w.split = reinterpret_cast<uint16_t *>(base + sl.split);
     }
     const int S = gridDim.x;
-    const int nf = A.F.n_fleets;
+    const int nf = B.F.n_fleets;
     for (int64_t b = blockIdx.x; b < nf; b += int64_t(64) * S) {
         const int64_t mine = b + int64_t(lane) * S;
-        uint64_t todo = __ballot(mine < nf && (A.want == 0 || A.fflag[mine] == 1));
+        uint64_t todo = __ballot(mine < nf && (A.want == 0 || B.fflag[mine] == 1));
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            sweep_fleet<kTables, kGlobal>(A, A.F, A.out, int(b + int64_t(bit) * S), w, Wave(lane));
+            sweep_fleet<kTables, kGlobal>(A, B.F, B.out, int(b + int64_t(bit) * S), w, Wave(lane));
         }
     }
 }
@@ -1315,8 +1328,11 @@ struct StepsDesc {
 struct StepsArgs {
     const StepsDesc *desc;
     int n_desc;
-    int first;  // (first item's batch) mod n_desc
+    int first;      // (first item's batch) mod n_desc
     int steps;
+    uint8_t *fflag;  // k-slot steps: per (group entry, fleet) hand-back flags, n_desc x n_fleets
+    unsigned *ctr;   // ... the launch's item counter (zeroed before it)
+    int next_off;    // ... the LDS byte offset of the workgroup's next-item slot
 };
 
 __device__ inline const __attribute__((address_space(4))) StepsDesc &steps_desc(const StepsArgs &G, int b) {
@@ -1463,11 +1479,11 @@ __global__ __launch_bounds__(64) void halda_resident_kernel(ResidentArgs R) {
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_kernel(SweepArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    sweep_body<true, false>(A, smem);
+    sweep_body<true, false>(A, batch_of(A), smem);
 }
 
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_big_kernel(SweepArgs A) {
-    sweep_body<true, true>(A, A.gtab + int64_t(blockIdx.x) * A.gstride);
+    sweep_body<true, true>(A, batch_of(A), A.gtab + int64_t(blockIdx.x) * A.gstride);
 }
 
 // halda_sweep_seg_kernel: fleets of at most kSegLanes devices (C2: 16) with at most kSegLanes
@@ -1593,9 +1609,9 @@ __device__ inline void kslot_put_records(KslotRecs *R, const KslotFleet &fd, int
     }
 }
 
-__device__ inline KslotFleet kslot_get_records(const SweepArgs &A, const KslotRecs *R, int f, int lane, int seg) {
+__device__ inline KslotFleet kslot_get_records(const SweepArgs &A, const halda_fleets &F, const KslotRecs *R, int f,
+                                               int lane, int seg) {
     KslotFleet fd;
-    const halda_fleets &F = A.F;
     fd.d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
     fd.M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - fd.d0);
     fd.me.alpha = R->alpha[lane]; fd.me.b = R->b[lane]; fd.me.p_bp = R->p_bp[lane]; fd.me.p_b = R->p_b[lane];
@@ -1612,10 +1628,9 @@ __device__ inline KslotFleet kslot_get_records(const SweepArgs &A, const KslotRe
     return fd;
 }
 
-__device__ inline KslotFleet kslot_records(const SweepArgs &A, int f, const Seg<kSegLanes> &sg) {
+__device__ inline KslotFleet kslot_records(const SweepArgs &A, const halda_fleets &F, int f, const Seg<kSegLanes> &sg) {
     KslotFleet fd;
     const int lane = sg.sl;
-    const halda_fleets &F = A.F;
     fd.d0 = A.uM > 0 ? int64_t(f) * A.uM + F.dev_off[0] : F.dev_off[f];
     fd.M = A.uM > 0 ? A.uM : int(F.dev_off[f + 1] - fd.d0);
     const DevFields mf = load_fields(F, fd.d0 + (lane < fd.M ? lane : 0));
@@ -1692,9 +1707,9 @@ __device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, int 
     }
 }
 
-__device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int j, int r1cap, int tabcap,
-                            const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk, unsigned long long *t_rec,
-                            const ScanSplit sp) {
+__device__ void sweep_kslot(const SweepArgs &A, const SweepBatch &B, const KslotFleet &fd, int f, int j, int r1cap,
+                            int tabcap, const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk,
+                            unsigned long long *t_rec, const ScanSplit sp) {
     using SG = Seg<kSegLanes>;
     constexpr int S = SG::S;
     const int lane = sg.sl;
@@ -1746,11 +1761,11 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
                 obj = obj + kappa;
                 st = HALDA_STATUS_OPTIMAL;
                 nl = n;
-                if (lane < M) put_xc(A, A.out, inst, M, lane, wl, n, sl, z, me);
+                if (lane < M) put_xc(A, B.out, inst, M, lane, wl, n, sl, z, me);
                 if (lane == 0 && (A.outs & kOutXC)) {
                     const int64_t at = xc_at(A, inst);
-                    if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
-                    if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
+                    if (at >= 0 && (A.outs & kOutX)) B.out.x[at + 7 * M] = hmax;
+                    if (at >= 0 && (A.outs & kOutC)) B.out.c[at + 7 * M] = kc;
                 }
             } else {
                 st = kSlotFlagged;  // a greedy fallback: the 64-lane table launch
@@ -1789,7 +1804,7 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
                         split_full(me, wl, g, n, sl);
                         dev_cycle(me, wl, n, sl, P, Q);
                         hmax = Q >= P ? 0.5 * (P + Q) : P;
-                        put_xc(A, A.out, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
+                        put_xc(A, B.out, inst, M, lane, wl, n, sl, Q > P ? 0.5 * (Q - P) : 0.0, me);
                     }
                     hmax = sg.max_f64(fmax(0.0, hmax));
                     obj = sg.sum_f64(0.0 + g) + kc * hmax;  // the segment kernel's sum (0.0 + g per lane)
@@ -1800,26 +1815,26 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
                     nl = n;
                     if (lane == 0 && (A.outs & kOutXC)) {
                         const int64_t at = xc_at(A, inst);
-                        if (at >= 0 && (A.outs & kOutX)) A.out.x[at + 7 * M] = hmax;
-                        if (at >= 0 && (A.outs & kOutC)) A.out.c[at + 7 * M] = kc;
+                        if (at >= 0 && (A.outs & kOutX)) B.out.x[at + 7 * M] = hmax;
+                        if (at >= 0 && (A.outs & kOutC)) B.out.c[at + 7 * M] = kc;
                     }
                 }
             }
         }
     }
     if (st == kSlotFlagged) {
-        flag_fleet(A, f, lane);
+        flag_fleet(A, B.fflag, f, lane);
     } else {
         if (lane == 0) {
-            if (A.outs & kOutObk) A.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
-            if (A.outs & kOutSt) A.out.status[inst] = st;
+            if (A.outs & kOutObk) B.out.obj_by_k[inst] = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
+            if (A.outs & kOutSt) B.out.status[inst] = st;
         }
         if ((A.outs & kOutXZ) && st != HALDA_STATUS_OPTIMAL && (A.outs & kOutXC)) {  // x / c of a non-optimal instance
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = lane; cc < 7 * M + 1; cc += S) {
-                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
-                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) B.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) B.out.c[at + cc] = 0.0;
                 }
         }
     }
@@ -1835,11 +1850,12 @@ __device__ void sweep_kslot(const SweepArgs &A, const KslotFleet &fd, int f, int
 
 // The pick of one fleet (segment lanes): best k over the slots in ascending k with strict "<", the
 // settled k's of no slot, best_k / obj_value / w / n and the fleet's flag byte.
-__device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const SlotPick *pk, const Seg<kSegLanes> &sg) {
+__device__ void kslot_pick(const SweepArgs &A, const SweepBatch &B, const SlotArgs &SA, int f, const SlotPick *pk,
+                           const Seg<kSegLanes> &sg) {
     constexpr int S = kSegLanes;
     const int lane = sg.sl;
-    const int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + A.F.dev_off[0] : A.F.dev_off[f];
-    const int M = A.uM > 0 ? A.uM : int(A.F.dev_off[f + 1] - d0);
+    const int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + B.F.dev_off[0] : B.F.dev_off[f];
+    const int M = A.uM > 0 ? A.uM : int(B.F.dev_off[f + 1] - d0);
     bool flagged = false;
     double best = kInf;
     int bq = -1;
@@ -1859,25 +1875,25 @@ __device__ void kslot_pick(const SweepArgs &A, const SlotArgs &SA, int f, const 
         if (slot) continue;
         const int64_t inst = int64_t(f) * A.n_k + jj;
         const int st = !(A.Ws[jj] < 1000000) ? HALDA_STATUS_UNSUPPORTED : HALDA_STATUS_INFEASIBLE;
-        if (A.outs & kOutObk) A.out.obj_by_k[inst] = kInf;
-        if (A.outs & kOutSt) A.out.status[inst] = st;
+        if (A.outs & kOutObk) B.out.obj_by_k[inst] = kInf;
+        if (A.outs & kOutSt) B.out.status[inst] = st;
         if ((A.outs & kOutXZ) && (A.outs & kOutXC)) {
             const int64_t at = xc_at(A, inst);
             if (at >= 0)
                 for (int cc = 0; cc < 7 * M + 1; ++cc) {
-                    if (A.outs & kOutX) A.out.x[at + cc] = 0.0;
-                    if (A.outs & kOutC) A.out.c[at + cc] = 0.0;
+                    if (A.outs & kOutX) B.out.x[at + cc] = 0.0;
+                    if (A.outs & kOutC) B.out.c[at + cc] = 0.0;
                 }
         }
     }
     if (lane == 0) {
-        A.out.best_k[f] = bq >= 0 ? A.ks[SA.j[bq]] : 0;
-        A.out.obj_value[f] = best;
-        A.fflag[f] = 0;
+        B.out.best_k[f] = bq >= 0 ? A.ks[SA.j[bq]] : 0;
+        B.out.obj_value[f] = best;
+        B.fflag[f] = 0;
     }
     if (lane < M) {
-        A.out.w[d0 + lane] = bq >= 0 ? pk[bq].w[lane] : 0;
-        A.out.n[d0 + lane] = bq >= 0 ? pk[bq].n[lane] : 0;
+        B.out.w[d0 + lane] = bq >= 0 ? pk[bq].w[lane] : 0;
+        B.out.n[d0 + lane] = bq >= 0 ? pk[bq].n[lane] : 0;
     }
 }
 
@@ -1975,30 +1991,41 @@ __device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const Kslot
     }
 }
 
-__global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The slot with the largest k > 1 tables (C2: k = 2): the workgroup's critical path, its threshold scan
+// the last thing running; -1 when no slot has tables.
+__device__ inline int kslot_crit(const SlotArgs &SA) {
+    int crit = -1, r1 = 0;
+    for (int p = 0; p < SA.n_slot; ++p)
+        if (SA.tab[p] > 0 && SA.r1[p] > r1) {
+            r1 = SA.r1[p];
+            crit = p;
+        }
+    return crit;
+}
+
+// One k-slot workgroup's four fleets (group g: fleets 4 g .. 4 g + 3 of batch B), every slot wave: the
+// records (wave 0, shared through LDS), the tables, each slot's solve and the split scan's parts, the
+// pick. Three workgroup barriers on every wave's path; the LDS areas are written only after the first
+// of them, so a workgroup may run one group after another.
+// ctr / next (k-slot steps launch): wave 0 takes the workgroup's next item from the launch's counter at
+// the start and posts it in LDS before the last barrier, where every wave reads it after the group.
+__device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepBatch &B, int64_t g,
+                            unsigned char *smem, int crit, unsigned *ctr = nullptr, int *next = nullptr) {
     constexpr int kPer = 64 / kSegLanes;
     const int lane = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // this wave's k-slot
     const Seg<kSegLanes> sg(lane);
     const int seg = lane / kSegLanes;
-    const int nf = A.F.n_fleets;
-    const int64_t f = int64_t(blockIdx.x) * kPer + seg;
+    const int nf = B.F.n_fleets;
+    const int64_t f = g * kPer + seg;
     SlotPick *pick = reinterpret_cast<SlotPick *>(smem + SA.pick_off);
-    // the slot with the largest k > 1 tables (C2: k = 2) is the workgroup's critical path: its
-    // threshold scan is the last thing running. It gets the SIMD's issue priority over the other
-    // slots' waves (of other workgroups) it shares the SIMD with.
-    int crit = -1;
-    {
-        int r1 = 0;
-        for (int p = 0; p < SA.n_slot; ++p)
-            if (SA.tab[p] > 0 && SA.r1[p] > r1) {
-                r1 = SA.r1[p];
-                crit = p;
-            }
-    }
-    if (q == crit) __builtin_amdgcn_s_setprio(3);  // (its helpers once their own slot is done)
+    // the critical slot's wave gets the SIMD's issue priority over the other slots' waves (of other
+    // workgroups) it shares the SIMD with (its helpers once their own slot is done)
+    if (q == crit) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);  // (a helper's raised priority ends with its group)
     SplitArea *split = reinterpret_cast<SplitArea *>(smem + SA.split_off) + seg;
+    unsigned nxt = 0;
+    if (ctr && q == 0 && lane == 0) nxt = atomicAdd(ctr, 1u);  // returns long before it is posted
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
     // XCC_ID[3:0] above
@@ -2011,12 +2038,12 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         KslotFleet fd = {};
         if (q == 0) {
             if (f < nf) {
-                fd = kslot_records(A, int(f), sg);
+                fd = kslot_records(A, B.F, int(f), sg);
                 kslot_put_records(recs, fd, lane, seg);
             }
         }
         __syncthreads();  // the records are in LDS
-        if (q != 0 && f < nf) fd = kslot_get_records(A, recs, int(f), lane, seg);
+        if (q != 0 && f < nf) fd = kslot_get_records(A, B.F, recs, int(f), lane, seg);
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
         if (f < nf) kslot_tables(A, SA, q, crit, fd, sg, smem, seg);
         const int my_part = kslot_part_of(SA, q);
@@ -2056,7 +2083,7 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0};
 #endif
         if (f < nf)
-            sweep_kslot(A, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
+            sweep_kslot(A, B, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
         if (q == SA.helper && f < nf && sg.sl == 0 && split->pub == 0) split->pub = 2;  // did not scan: helpers skip
         if (q == SA.check_wave) kslot_check(A, SA, fd, split, sg, smem, seg, f < nf);
         if (my_part) {  // after its own slot, at the split slot's priority
@@ -2069,10 +2096,59 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
         HALDA_KSTAMPW(10, t_rec[5]);
     }
     HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
+    if (ctr && q == 0 && lane == 0) *next = int(nxt);
     __syncthreads();
     HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
-    if (q == 0 && f < nf) kslot_pick(A, SA, int(f), pick + seg * SA.n_slot, sg);
+    if (q == 0 && f < nf) kslot_pick(A, B, SA, int(f), pick + seg * SA.n_slot, sg);
     HALDA_KSTAMPW(4, __builtin_amdgcn_s_memtime());
+}
+
+__global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    kslot_group(A, SA, batch_of(A), int64_t(blockIdx.x), smem, kslot_crit(SA));
+}
+
+// halda_sweep_kslot_steps_kernel: `steps` batches of k-slot sweeps (C2 shapes) in one launch, the
+// group launch's k-slot form. Items (batch t, group of four fleets) in batch order, taken from a counter
+// one at a time by the resident workgroups, so a workgroup that ends a group early takes the next one at
+// once: the launch is paced by the mean group, not by the slowest of the 1,024 resident at once. Item
+// (t, gg) solves group g = (gg + t * kKslotRot) mod n_groups (a bijection per batch), which spreads a
+// slow group's batches over the launch. Fleets a slot flags go to the per-batch
+// flag array; halda_sweep_tables_steps_kernel redoes them after the launch.
+constexpr int kKslotRot = 389;
+
+__global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_steps_kernel(SweepArgs A, SlotArgs SA, StepsArgs G) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int crit = kslot_crit(SA);
+    const int nf = A.F.n_fleets;
+    const int ng = (nf + 64 / kSegLanes - 1) / (64 / kSegLanes);
+    const int items = G.steps * ng;
+    // the next item: from the launch's counter (zeroed before the launch), so a workgroup that ends a
+    // group early takes the next one at once; the slot past the k-slot LDS areas carries it to the waves
+    int *next = reinterpret_cast<int *>(smem + G.next_off);
+    if (threadIdx.x == 0) *next = int(atomicAdd(G.ctr, 1u));
+    __syncthreads();
+    int i = *next;
+    while (i < items) {
+        const int t = i / ng, gg = i - t * ng;
+        const int g = int((int64_t(gg) + int64_t(t) * kKslotRot) % ng);
+        const int b = int((int64_t(G.first) + t) % G.n_desc);
+        const halda_fleets F = steps_fleets(steps_desc(G, b));
+        const FleetOut O = steps_out(steps_desc(G, b));
+        kslot_group(A, SA, SweepBatch{F, O, G.fflag + int64_t(b) * nf}, g, smem, crit, G.ctr, next);
+        i = *next;  // posted before the group's last barrier
+    }
+}
+
+// The gated table launch behind a k-slot steps launch: blockIdx.y = the group entry (first + y) mod
+// n_desc, the fleets its items flagged (gated on the launch's hand-back flag).
+__global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_steps_kernel(SweepArgs A,
+                                                                                                StepsArgs G) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int b = int((int64_t(G.first) + blockIdx.y) % G.n_desc);
+    const halda_fleets F = steps_fleets(steps_desc(G, b));
+    const FleetOut O = steps_out(steps_desc(G, b));
+    sweep_body<true, false>(A, SweepBatch{F, O, G.fflag + int64_t(b) * A.F.n_fleets}, smem);
 }
 
 // halda_pick_kernel: one wave per fleet. obj_value per k = c.x + sum t_comm +

@@ -104,11 +104,11 @@ def test_group_batches_see_in_place_rewrites(llama_online_model):
     group.close()
 
 
-@pytest.mark.parametrize("M,persistent", [(16, False), (70, False), (12, True)])
+@pytest.mark.parametrize("M,persistent", [(16, True), (70, False), (12, True)])
 def test_group_other_shapes(llama_online_model, M, persistent):
-    """Shapes the steps kernel does not take run batch by batch (C2's k > 1 tables: the k-slot launch;
-    fleets wider than 64 devices); M = 12 at L = 12 opens only k = 1 and W = M, so it is a register sweep.
-    Either way every batch's results equal its own solve."""
+    """C2's k > 1 tables (16 devices) run as the k-slot form of the steps launch
+    (halda_sweep_kslot_steps_kernel); fleets wider than 64 devices batch by batch; M = 12 at L = 12 opens
+    only k = 1 and W = M, so it is a register sweep. Either way every batch's results equal its own solve."""
     import torch
 
     from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup
@@ -164,3 +164,43 @@ def test_plans_and_groups_fail_cleanly_after_the_context_is_freed(llama_online_m
     assert rc != 0
     group.close()
     dt.replan()
+
+
+@pytest.mark.parametrize("first,steps", [(0, 7), (2, 20)])
+def test_kslot_group_launch_with_hand_backs(llama_online_model, first, steps):
+    """The k-slot form of the group launch on fleets of 1..16 devices (one-device fleets and k = 1
+    fast-path fallbacks are flagged by the k-slot items and redone per batch by the gated
+    halda_sweep_tables_steps_kernel): three tables (the same layout, perturbed values), more batches than
+    tables; every table's statuses, per-k objectives, best k, obj_value, w, n equal its own solve."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup
+
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    sizes = [1 + (s * 7) % 16 for s in range(300)]
+    base = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(35000 + s, M)]
+                        for s, M in enumerate(sizes)], llama_online_model)
+    tabs, wants = [], []
+    for t in range(3):
+        table = base.perturbed(np.random.default_rng(70 + t)) if t else base
+        wants.append(solve_table(table, llama_online_model, KS, 0.5))
+        tabs.append(DeviceFleetTable(table, llama_online_model, KS, 0.5, dev, want_per_k=True))
+    group = PlanGroup(tabs, ctx)
+    assert group.persistent
+    for t in tabs:
+        for v in t.out.values():
+            v.zero_()
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    ctx.set_timing(True)
+    try:
+        group.launch(first, steps, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ms = ctx.last_fleet_ms()
+    finally:
+        ctx.set_timing(False)
+    assert "halda_sweep_kslot_kernel" in ms and "halda_sweep_tables_kernel" in ms, ms
+    for d, w in zip(tabs, wants):
+        _check(d, w, True)
+    group.close()
