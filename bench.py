@@ -333,15 +333,15 @@ def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None, workload="c3")
             "launch_ms": phase_ms}
 
 
-def group_roofline(launch_ms, steps, batch_bytes, n_fleets, single):
+def group_roofline(launch_ms, steps, batch_bytes, n_fleets, single, kern="halda_sweep_steps_kernel",
+                   workload="c3_steps"):
     """Roofline of the headline's launch as launched: ONE halda_sweep_steps_kernel launch of `steps`
     batches, algorithmic bytes = steps x one batch's, time = HIP events around that launch
     on its stream; HBM traffic and the VALU count from this build's rocprofv3 profiles (per launch of
     the same K). `single` (the per-batch kernel's own roofline, one launch per batch) is kept beside it."""
     alg = steps * batch_bytes
     achieved = alg / (launch_ms * 1e-3) / 1e9
-    kern = "halda_sweep_steps_kernel"
-    vp = valu_profile(kern, "c3_steps")
+    vp = valu_profile(kern, workload)
     if vp and vp.get("items"):
         # VALU per (fleet, batch) item of the profiled launch, times this launch's items
         need = vp["valu_per_wave"] * vp["waves"] / vp["items"] * (steps * n_fleets) * VALU_CYCLES / (
@@ -604,8 +604,10 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
         "ms_per_step_one_stream": ev1, "instances_per_s_one_stream": inst / (ev1 * 1e-3),
         "ms_per_step_two_streams": el2 / steps * 1e3, "instances_per_s_two_streams": inst * steps / el2,
         "steps": steps, "resident_copies": n,
-        "roofline": roofline(ph, {k: alg for k in ph}, pmc_traffic, ev1 if single_launch_steps(ph) else None,
-                             workload="c2"),
+        "roofline": group_roofline(evg, steps, alg, C3_FLEETS,
+                                   roofline(ph, {k: alg for k in ph}, pmc_traffic,
+                                            ev1 if single_launch_steps(ph) else None, workload="c2"),
+                                   kern="halda_sweep_kslot_steps_kernel", workload="c2_steps"),
     }
 
 

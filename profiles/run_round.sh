@@ -35,6 +35,9 @@ echo "[prof] sq steps"
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS \
     --kernel-trace --output-format csv -d "$OUT/valu_steps" -o run -- \
     python3 tools/steps_profile.py --steps 20 --single 0 > "$OUT/valu_steps.log" 2>&1
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS \
+    --kernel-trace --output-format csv -d "$OUT/valu_steps16" -o run -- \
+    python3 tools/steps_profile.py --steps 20 --single 0 --M 16 > "$OUT/valu_steps16.log" 2>&1
 python3 tools/valu_stamp.py "$R" c3="$OUT/valu_m64/run_counter_collection.csv" c2="$OUT/valu_m16/run_counter_collection.csv" \
-    c3_steps="$OUT/valu_steps/run_counter_collection.csv:81920" > /dev/null
+    c3_steps="$OUT/valu_steps/run_counter_collection.csv:81920" c2_steps="$OUT/valu_steps16/run_counter_collection.csv:81920" > /dev/null
 echo "[prof] done"

@@ -75,7 +75,7 @@ def main(R):
             "FETCH_SIZE_KB": fk, "WRITE_SIZE_KB": wk,
             "hbm_bytes_per_launch": fk * 1024 / f8 + wk * 1024,
         }
-        if name == "halda_sweep_steps_kernel":  # one launch = K batches (run_round.sh: the bench's --steps)
+        if name in ("halda_sweep_steps_kernel", "halda_sweep_kslot_steps_kernel"):  # one launch = K batches
             e = out["kernels"][name]
             e["steps"] = STEPS
             e["hbm_bytes_per_batch"] = e["hbm_bytes_per_launch"] / STEPS
