@@ -104,7 +104,7 @@ RES = 4 + 8 + 8 + 8 + 8  # status, obj_lin, dual_bound, gap, nodes
 DEV_FIELDS = 10 * 8 + 6 * 8 + 2  # FleetTable bytes per device (f64 x 10, int64 x 6, os_class, flags)
 
 
-def algorithmic_bytes(lowered, refs, n_k: int):
+def algorithmic_bytes(lowered, refs, n_k: int, settled=None):
     """Bytes each launch must move, {kernel: bytes per launch}, for the lowered batch
     `lowered` (host lowering of the same fleets, one FleetMILP per fleet) and its instances `refs`.
 
@@ -117,14 +117,16 @@ def algorithmic_bytes(lowered, refs, n_k: int):
     objective offsets and per instance its header plus, for W >= M, every column / row vector, for
     W < M (the screen settles it) the w bounds, the C column and the equality-row bounds; pick: per
     instance its status, per optimal instance its header, c and x, per fleet the offsets in and best k,
-    obj_value and w / n out, obj_by_k / status when requested (not in the bench)."""
+    obj_value and w / n out, obj_by_k / status when requested (not in the bench). `settled` (one flag per
+    instance, halda_solve_batch_device_settled): a settled instance costs the screen its header, its flag,
+    its verdict byte and the result scalars."""
     solve = screen = lower = pick = 0
     fleets_seen, fleets_solved = set(), set()
-    for ref in refs:
+    for i, ref in enumerate(refs):
         fl = lowered[ref.fleet]
         M, nc, nr = fl.M, fl.n_cols, fl.n_rows
         csr = 4 * (nr + 1) + 12 * fl.nnz
-        scr = HDR + 8 + 12 * M + 16 + 8 * M + 8 + 1
+        scr = HDR + 1 + 1 if settled is not None and settled[i] else HDR + 8 + 12 * M + 16 + 8 * M + 8 + 1
         screen += scr
         if ref.fleet not in fleets_seen:
             fleets_seen.add(ref.fleet)
@@ -749,7 +751,7 @@ def main():
             return 2
 
     from distilp_amd.solver._libhalda import get_context
-    from distilp_amd.solver.batch import assemble
+    from distilp_amd.solver.batch import assemble, settled_instances
     from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup, PlanRotation, fleet_table
     from distilp_amd.solver.lower import lower_fleet
 
@@ -806,18 +808,24 @@ def main():
     n_so = args.copies or 2
     copies = [to_device(batch, torch, dev) for _ in range(n_so)]
     cptrs = [({f: t.data_ptr() for f, t in k.items()}, {f: t.data_ptr() for f, t in o.items()}) for k, o in copies]
+    # the lowering's own verdicts: the bound-infeasible k's (M > W = L / k), computed with the lowering
+    # (set-up, like the CSR) and handed to halda_solve_batch_device_settled, which then reads none of
+    # their rows; every step still writes all results
+    settled = settled_instances(batch)
+    settled_dev = torch.from_numpy(settled).to(dev)
+    hint = [settled_dev.data_ptr()]
 
     def solve_step():
         # consecutive batches alternate over the streams too (per-stream scratch: the next batch's
         # screen overlaps the previous batch's k = 1 solves)
         ptrs, optrs = cptrs[turn[1] % n_so]
-        ctx.solve_device(ptrs, batch, optrs, stream=srefs[turn[1] % len(srefs)])
+        ctx.solve_device(ptrs, batch, optrs, stream=srefs[turn[1] % len(srefs)], settled=hint[0])
         turn[1] += 1
 
     def solve_step_one_stream():
         ptrs, optrs = cptrs[turn[1] % n_so]
         turn[1] += 1
-        ctx.solve_device(ptrs, batch, optrs, stream=sref)
+        ctx.solve_device(ptrs, batch, optrs, stream=sref, settled=hint[0])
 
     setup_s = time.perf_counter() - t_setup
 
@@ -862,6 +870,10 @@ def main():
                                  for _ in range(3))
     el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
     el_solve1 = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
+    hint[0] = None  # the same legs without the settled flags: the screen proves every verdict itself
+    el_solve_ns = timed(solve_step, args.steps, torch, dev, dist, world)
+    el_solve1_ns = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
+    hint[0] = settled_dev.data_ptr()
     el_strong = None
     if world > 1 and not strong_head:
         s_seeds = fleet_seeds(args, rank, world, True)
@@ -900,6 +912,7 @@ def main():
     fl_mean = {k: statistics.mean(p.get(k, 0.0) for p in fl_ms) for k in fl_ms[0]}
     so_mean = {k: statistics.mean(p[k] for p in so_ms) for k in so_ms[0]}
     alg = algorithmic_bytes(lowered, refs, len(ks))
+    alg_so = algorithmic_bytes(lowered, refs, len(ks), settled)
 
     inst_rank = len(fleets) * len(ks)
     total = inst_rank * world * args.steps if not strong_head else C3_FLEETS * len(ks) * args.steps
@@ -960,15 +973,20 @@ def main():
             "roofline": group_roofline(group_ms, args.steps, alg["halda_sweep_kernel"], len(fleets),
                                        roofline(fl_mean, alg, pmc_traffic, sweep_ev_ms)),
             "solve_only": {
-                "what": "same fleets lowered on the host beforehand; halda_solve_batch_device on the CSR batch "
+                "what": "same fleets lowered on the host beforehand, the lowering's bound-infeasible k's (M > "
+                        "L/k) passed as settled flags; halda_solve_batch_device_settled on the CSR batch "
                         "resident in HBM (the milp() replacement alone); consecutive batches alternate over the "
-                        "streams like the headline (ms_per_step_one_stream: all on one stream)",
+                        "streams like the headline (ms_per_step_one_stream: all on one stream; *_no_settled: "
+                        "halda_solve_batch_device, the screen proving every verdict itself)",
                 "instances_per_s": inst_rank * world * args.steps / el_solve,
                 "ms_per_step": el_solve / args.steps * 1e3,
                 "ms_per_step_one_stream": el_solve1 / args.steps * 1e3,
+                "ms_per_step_no_settled": el_solve_ns / args.steps * 1e3,
+                "ms_per_step_one_stream_no_settled": el_solve1_ns / args.steps * 1e3,
+                "settled_per_step": int(settled.sum()),
                 "streams": len(srefs),
                 "resident_copies": n_so,
-                "roofline": roofline(so_mean, alg, pmc_traffic),
+                "roofline": roofline(so_mean, alg_so, pmc_traffic),
             },
             "strong": None if el_strong is None else {
                 "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,

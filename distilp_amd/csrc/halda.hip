@@ -277,7 +277,8 @@ int sweep_slot(Ctx *c, hipStream_t s, int64_t nf, Ctx::SweepSlot **out) {
     return HALDA_OK;
 }
 
-int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t stream) {
+int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t stream,
+           const uint8_t *settled = nullptr) {
     if (in.n_inst <= 0) return HALDA_OK;
     if (in.max_cols < 1 || in.max_R1 < 1 || in.max_tab < 0 || in.max_tab_kc < 0)
         return fail(HALDA_E_ARG, "halda_batch shape summary (max_cols/max_R1/max_tab/max_tab_kc) not set");
@@ -331,7 +332,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         // screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc));
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc), settled);
         HIP_TRY(hipGetLastError());
         if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
         int per_cu = 0;
@@ -1075,6 +1076,15 @@ int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     return launch(c, *in, *out, s);
+}
+
+int halda_solve_batch_device_settled(void *ctx, const halda_batch *in, halda_result *out, const uint8_t *settled,
+                                     void *stream) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c || !in || !out) return fail(HALDA_E_ARG, "NULL ctx/in/out");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    return launch(c, *in, *out, s, settled);
 }
 
 int halda_last_kernel_ms(void *ctx, double *ms) {

@@ -60,7 +60,8 @@ struct ScreenOut {
 };
 
 __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i0, int lane,
-                                    int mmax, int r1max, int tab, int tab_kc, ScreenOut &so) {
+                                    int mmax, int r1max, int tab, int tab_kc, ScreenOut &so,
+                                    const uint8_t *settled = nullptr) {
     // lane g < kScreenPer: header of instance i0 + g. Loads are branch-free (lanes
     // without an instance read a valid element and discard it) so that each round
     // trip's loads issue before the first wait.
@@ -69,18 +70,35 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     const int64_t mc = own ? my : i0;
     const int N0 = B.n_cols[mc], m0 = B.n_rows[mc];
     const int64_t co0 = B.col_off[mc], ro0 = B.row_off[mc], cs0 = B.csr_off[mc];
+    // a settled instance (the caller's proof of bound infeasibility, halda_solve_batch_device_settled) is
+    // INFEASIBLE as it stands: none of its rows or bounds is read (only its header)
+    const bool hint = own && settled && settled[mc] != 0;
     const int N = own ? N0 : 1, m = own ? m0 : 1;
     const int64_t co = own ? co0 : 0, ro = own ? ro0 : 0, cs = own ? cs0 : 0;
-    int status = 0;  // 0 = still open
-    if (N < 1 || (N - 1) % 7 != 0 || m < 1) status = HALDA_STATUS_UNSUPPORTED;
+    int status = hint ? HALDA_STATUS_INFEASIBLE : 0;  // 0 = still open
+    if (!status && (N < 1 || (N - 1) % 7 != 0 || m < 1)) status = HALDA_STATUS_UNSUPPORTED;
     const int M = status ? 0 : (N - 1) / 7;
     if (!status && M > mmax) status = HALDA_STATUS_TOO_LARGE;
-    // round trip 2: equality-row extent and bounds, c[C] (lane g)
-    const int ma = max(m0, 1);
-    const int32_t *rp = B.row_ptr + cs0;
-    const int eqs0 = rp[ma - 1], eqe0 = rp[ma];
-    const double Wd0 = B.row_ub[ro0 + ma - 1], Wl0 = B.row_lb[ro0 + ma - 1];
-    const double cC0 = B.c[co0 + 7 * int64_t(max(M, 0))];
+    // round trip 2: equality-row extent and bounds, c[C] (lane g). Lanes without an unsettled instance
+    // read the lines of the first lane that has one; a wave of settled instances alone reads nothing.
+    const bool rd = own && !hint;
+    const uint64_t rdm = __ballot(rd);
+    const int src = rdm ? __builtin_ctzll(rdm) : 0;
+    const int m_r = __shfl(m0, src), M_r = __shfl(M, src);
+    const int64_t cs_r = shfl64(cs0, src), ro_r = shfl64(ro0, src), co_r = shfl64(co0, src);
+    const int ma = max(rd ? m0 : m_r, 1);
+    const int32_t *rp = B.row_ptr + (rd ? cs0 : cs_r);
+    const int64_t rr = (rd ? ro0 : ro_r) + ma - 1;
+    const int64_t ci = (rd ? co0 : co_r) + 7 * int64_t(max(rd ? M : M_r, 0));
+    int eqs0 = 0, eqe0 = 0;
+    double Wd0 = 0.0, Wl0 = 0.0, cC0 = 0.0;
+    if (rdm) {
+        eqs0 = rp[ma - 1];
+        eqe0 = rp[ma];
+        Wd0 = B.row_ub[rr];
+        Wl0 = B.row_lb[rr];
+        cC0 = B.c[ci];
+    }
     const bool live = own && !status;
     const int eqs = live ? eqs0 : 0, eqe = live ? eqe0 : 0;
     const double Wd = live ? Wd0 : 0.0, Wl = live ? Wl0 : 0.0, cC = live ? cC0 : 0.0;
@@ -2274,12 +2292,13 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
 
 // Screen: four waves per workgroup, each screening kScreenPer consecutive instances.
 __global__ __launch_bounds__(256) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls, int mmax,
-                                                           int r1max, int tab, int tab_kc) {
+                                                           int r1max, int tab, int tab_kc,
+                                                           const uint8_t *settled) {
     const int lane = threadIdx.x & 63;
     const int64_t i0 = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kScreenPer;
     if (i0 >= B.n_inst) return;
     ScreenOut so;
-    screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so);
+    screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so, settled);
 }
 
 // k = 1 fast path: persistent 64-thread workgroups (one wave each) over the

@@ -76,7 +76,8 @@ class HaldaResultC(ctypes.Structure):
     ]
 
 
-EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device", "halda_last_kernel_ms",
+EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batch_device",
+           "halda_solve_batch_device_settled", "halda_last_kernel_ms",
            "halda_last_solve_kernel_ms", "halda_last_phase_ms", "halda_lds_bytes", "halda_last_error", "halda_free",
            "halda_solve_fleets", "halda_solve_fleets_host", "halda_last_lowered", "halda_set_timing",
            "halda_last_fleet_ms", "halda_set_fleets_path", "halda_init_multi", "halda_solve_fleets_multi",
@@ -129,6 +130,10 @@ def load_library(path: Path | str | None = None):
         lib.halda_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC),
                                                  ctypes.POINTER(HaldaResultC), ctypes.c_void_p]
         lib.halda_solve_batch_device.restype = ctypes.c_int
+        lib.halda_solve_batch_device_settled.argtypes = [ctypes.c_void_p, ctypes.POINTER(HaldaBatchC),
+                                                         ctypes.POINTER(HaldaResultC), ctypes.c_void_p,
+                                                         ctypes.c_void_p]
+        lib.halda_solve_batch_device_settled.restype = ctypes.c_int
         lib.halda_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.halda_last_kernel_ms.restype = ctypes.c_int
         lib.halda_last_solve_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
@@ -262,8 +267,10 @@ class HaldaContext:
         return out
 
     def solve_device(self, dev_ptrs: Dict[str, int], b: HostBatch, out_ptrs: Dict[str, int],
-                     stream: Optional[int] = None) -> None:
-        """halda_solve_batch_device: arrays already resident in HBM (e.g. torch tensors)."""
+                     stream: Optional[int] = None, settled: Optional[int] = None) -> None:
+        """halda_solve_batch_device: arrays already resident in HBM (e.g. torch tensors). `settled`: the
+        device address of n_inst bytes marking instances the caller proved bound-infeasible
+        (halda_solve_batch_device_settled; batch.settled_instances computes them from a host batch)."""
         s = HaldaBatchC()
         s.n_inst = b.n_inst
         s.max_cols, s.max_R1, s.max_tab, s.max_tab_kc = b.max_cols, b.max_R1, b.max_tab, b.max_tab_kc
@@ -273,8 +280,12 @@ class HaldaContext:
         s.time_limit = 3600.0
         r = HaldaResultC(**{k: int(v) for k, v in out_ptrs.items()})
         with self._lock:  # one launch at a time per context (verdict bytes, hand-back flag)
-            rc = self.lib.halda_solve_batch_device(self.ctx, ctypes.byref(s), ctypes.byref(r),
-                                                   ctypes.c_void_p(stream) if stream else None)
+            st = ctypes.c_void_p(stream) if stream else None
+            if settled:
+                rc = self.lib.halda_solve_batch_device_settled(self.ctx, ctypes.byref(s), ctypes.byref(r),
+                                                               ctypes.c_void_p(int(settled)), st)
+            else:
+                rc = self.lib.halda_solve_batch_device(self.ctx, ctypes.byref(s), ctypes.byref(r), st)
         if rc != 0:
             raise RuntimeError(f"halda_solve_batch_device failed ({rc}): {last_error(self.lib)}")
 

@@ -89,3 +89,40 @@ def assemble(fleets: Sequence[FleetMILP], ks: Sequence[Sequence[int]], mip_gap: 
         max_cols=max_cols, max_R1=max_R1, max_tab=max_tab, max_tab_kc=max_tab_kc, mip_rel_gap=float(mip_gap or 0.0),
     )
     return batch, refs
+
+
+def settled_instances(b: HostBatch) -> np.ndarray:
+    """The bound-infeasible instances of a host batch, one byte each (1 = settled), for
+    halda_solve_batch_device_settled: instance i is settled when it is a HALDA instance (N = 7M + 1
+    columns, the last row an equality sum_j w_j = W with integral W in [0, 1e6), its entries the first M
+    columns with coefficient 1) and its w lower bounds prove infeasibility -- a bound below 0, a ceil above
+    W, or ceilings summing past W (NaN bounds count 0, as on the GPU). That is the screen's own verdict
+    (HiGHS's presolve answer for M > W = L / k, res.success == False in halda_p_solver.py:369-436), so the
+    settled call writes the same results while reading none of these instances' rows."""
+    n = b.n_inst
+    N = b.n_cols.astype(np.int64)
+    m = b.n_rows.astype(np.int64)
+    ok = (N >= 1) & ((N - 1) % 7 == 0) & (m >= 1)
+    M = np.where(ok, (N - 1) // 7, 0)
+    eq = np.where(ok, b.row_off + m - 1, 0)
+    W = b.row_ub[eq]
+    Wl = b.row_lb[eq]
+    with np.errstate(invalid="ignore"):
+        ok &= (Wl == W) & (W >= 0.0) & (W < 1e6) & (W == np.floor(W))
+    rs = b.row_ptr[np.where(ok, b.csr_off + m - 1, 0)].astype(np.int64)
+    re = b.row_ptr[np.where(ok, b.csr_off + m, 0)].astype(np.int64)
+    ok &= (re - rs == M) & (M > 0)
+    Mo = np.where(ok, M, 0)
+    inst = np.repeat(np.arange(n), Mo)
+    j = np.arange(int(Mo.sum())) - np.repeat(np.cumsum(Mo) - Mo, Mo)
+    e = rs[inst] + j
+    bad = (b.col_idx[e] != j) | (b.val[e] != 1.0)
+    ok &= np.bincount(inst, weights=bad, minlength=n) == 0
+    lb = b.col_lb[b.col_off[inst] + j]
+    with np.errstate(invalid="ignore"):
+        up = np.ceil(lb)
+        nan = np.isnan(lb)
+        hit = ~nan & ((lb < 0.0) | (up > W[inst]))
+        up = np.where(nan, 0.0, up)
+    infeas = (np.bincount(inst, weights=hit, minlength=n) > 0) | (np.bincount(inst, weights=up, minlength=n) > W)
+    return (ok & infeas).astype(np.uint8)

@@ -117,6 +117,19 @@ int halda_solve_batch(void *ctx, const halda_batch *in, halda_result *out);
  * enqueued on `stream` (a hipStream_t; NULL = the context's stream). */
 int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out, void *stream);
 
+/* halda_solve_batch_device with the caller's settled instances: settled[i] != 0
+ * (a DEVICE array of n_inst bytes) states that the caller has already proved
+ * instance i bound-infeasible (sum_j ceil(lb(w_j)) > W, e.g. M devices of w >= 1
+ * over W = L/k < M layers: the k's milp() returns res.success == False,
+ * halda_p_solver.py:369-436). Its result is written as HALDA_STATUS_INFEASIBLE
+ * (the screen's own verdict for it: obj_lin = dual_bound = gap = inf, nodes 0)
+ * and none of its rows or column bounds is read; only its header entries are.
+ * settled[i] == 0 instances are solved as by halda_solve_batch_device, bit for
+ * bit; settled == NULL is halda_solve_batch_device. A settled flag on an
+ * instance that is not infeasible is the caller's error (it is not checked). */
+int halda_solve_batch_device_settled(void *ctx, const halda_batch *in, halda_result *out, const uint8_t *settled,
+                                     void *stream);
+
 /* Device time of the last solve's kernel sequence (both launches) in ms. */
 int halda_last_kernel_ms(void *ctx, double *ms);
 
