@@ -325,14 +325,15 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     }
     uint8_t *cls = slot->cls;
     int *hb_flag = slot->hb;
-    const int launch_id = ++ctx->launch_id;  // tags this launch's k = 1 hand-backs (no reset needed)
+    int *gen_flag = slot->hb + 16;  // its own 64 B of the slot's flag block
+    const int launch_id = ++ctx->launch_id;  // tags this launch's flags: k = 1 hand-backs, k > 1 work (no reset)
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
     {
         // screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
-                           cls, mmax, in.max_R1, int(tab), int(tab_kc), settled);
+                           cls, mmax, in.max_R1, int(tab), int(tab_kc), settled, gen_flag, launch_id);
         HIP_TRY(hipGetLastError());
         if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
         int per_cu = 0;
@@ -355,8 +356,10 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_kernel), lds_kc, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
+        // gated on the screen's flag: a batch whose k > 1 instances were all settled by the screen (C3:
+        // every k > 1 is bound-infeasible) leaves this launch nothing to do
         hipLaunchKernelGGL(halda_solve_kernel, dim3(grid), dim3(64), size_t(lds_kc), stream, in, out, cls, ls.mmax,
-                           ls.r1, 0, ls.tab_kc, static_cast<const int *>(hb_flag), launch_id, 0, int(CLS_GEN));
+                           ls.r1, 0, ls.tab_kc, static_cast<const int *>(gen_flag), launch_id, 1, int(CLS_GEN));
         HIP_TRY(hipGetLastError());
     }
     {

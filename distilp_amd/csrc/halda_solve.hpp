@@ -61,7 +61,7 @@ struct ScreenOut {
 
 __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i0, int lane,
                                     int mmax, int r1max, int tab, int tab_kc, ScreenOut &so,
-                                    const uint8_t *settled = nullptr) {
+                                    const uint8_t *settled, int *gen_flag, int launch_id) {
     // lane g < kScreenPer: header of instance i0 + g. Loads are branch-free (lanes
     // without an instance read a valid element and discard it) so that each round
     // trip's loads issue before the first wait.
@@ -202,6 +202,8 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     so.ro = ro;
     so.cs = cs;
     so.verdict = own ? verdict : CLS_DONE;
+    // the k > 1 general launch of this batch has work (it is gated on this flag)
+    if (__ballot(own && verdict == CLS_GEN) && lane == 0) *gen_flag = launch_id;
     if (own) {
         cls[my] = uint8_t(verdict);
         if (verdict == CLS_DONE) {
@@ -1618,7 +1620,8 @@ __device__ inline void solve_general(halda_batch B, halda_result Rz, uint8_t *cl
                                      int tab_kc, const int *hb_flag, int launch_id, int gated, int want,
                                      unsigned char *slice_base) {
     const int lane = threadIdx.x;
-    // gated: no k > 1 or wide instance in the batch; only k = 1 hand-backs (flagged) can be here
+    // gated: only flagged work can be here -- k = 1 hand-backs (no k > 1 or wide instance in the batch), or
+    // the k > 1 instances the screen flagged (the k > 1 launch of launch())
     if (gated && __hip_atomic_load(hb_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != launch_id) return;
     const Slice sl = make_slice(mmax, r1max, tab, tab_kc);
     unsigned char *base = slice_base;
@@ -1988,7 +1991,7 @@ constexpr int kRpSlots = 5;  // row pointers rp[0 .. ncap] per lane: ncap <= 64 
 // registers. Fills d. Returns 0 ok, 1 not a HALDA MILP, 2 not in this shape
 // (the caller then runs the generic decode).
 __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *scol_raw, unsigned char *sval_raw,
-                         const Inst &I, int lane, Dev &d, int &sumlo) {
+                         Inst &I, int lane, Dev &d, int &sumlo) {
     const int M = I.M, ncyc = 2 * M, ncap = I.m - 1 - ncyc;
     // M >= 4: the staged 16-B chunks past a segment's end stay inside the equality row
     if (M < 4 || ncap < 0 || ncap > 64 * kCapSlots || ncyc > 64 * kCycSlots) return 2;
@@ -2021,6 +2024,10 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
         rlb[j] = B.row_lb[I.ro + r];
     }
     const int cbase = I.rp[0], cend = I.rp[ncap];
+    // the equality row's rhs W and c[C] (the caller has only the header): in this round trip too
+    I.Wd = B.row_ub[I.ro + I.m - 1];
+    I.kc = B.c[co + I.iC];
+    I.W = int(I.Wd);
     int dbad = iz != 0 || cz != 0.0 || lz != 0.0 || uz != kInf || lbv[1] < 0.0;
 #pragma unroll
     for (int b = 0; b < 6; ++b) dbad |= ig[b] != 1;
@@ -2219,7 +2226,7 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
 // One k = 1 instance (lane = device) from decode to x; hands the instance to the
 // general kernel (cls = CLS_GEN) when the fast path does not apply.
 __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w,
-                         unsigned char *scol, unsigned char *sval, const Inst &I, int lane, int *hb_flag,
+                         unsigned char *scol, unsigned char *sval, Inst I, int lane, int *hb_flag,
                          int launch_id) {
     HALDA_STAMP(0);
     Dev d = {};
@@ -2290,15 +2297,35 @@ __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *
     HALDA_STAMP(6);
 }
 
+// One k = 1 instance of the fast path from its header (decode_k1 loads W and c[C] with its first round
+// trip).
+__device__ inline void k1_instance(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w,
+                                   unsigned char *scol, unsigned char *sval, int lane, int *hb_flag, int launch_id,
+                                   int64_t inst, int N, int m, int64_t co, int64_t ro, int64_t cs) {
+    Inst I;
+    I.inst = int(inst);
+    I.m = m;
+    I.M = (N - 1) / 7;
+    I.iC = 7 * I.M;
+    I.invM = 1.0f / float(I.M);
+    I.co = co;
+    I.ro = ro;
+    I.rp = B.row_ptr + cs;
+    I.Wd = 0.0;
+    I.W = 0;
+    I.kc = 0.0;
+    solve_k1(B, Rz, cls, w, scol, sval, I, lane, hb_flag, launch_id);
+}
+
 // Screen: four waves per workgroup, each screening kScreenPer consecutive instances.
 __global__ __launch_bounds__(256) void halda_screen_kernel(halda_batch B, halda_result Rz, uint8_t *cls, int mmax,
                                                            int r1max, int tab, int tab_kc,
-                                                           const uint8_t *settled) {
+                                                           const uint8_t *settled, int *gen_flag, int launch_id) {
     const int lane = threadIdx.x & 63;
     const int64_t i0 = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kScreenPer;
     if (i0 >= B.n_inst) return;
     ScreenOut so;
-    screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so, settled);
+    screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so, settled, gen_flag, launch_id);
 }
 
 // k = 1 fast path: persistent 64-thread workgroups (one wave each) over the
@@ -2323,20 +2350,9 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_ke
         while (todo) {
             const int bit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            Inst I;
-            I.inst = int(base + int64_t(bit) * S);
-            const int N = B.n_cols[I.inst];
-            I.m = B.n_rows[I.inst];
-            I.M = (N - 1) / 7;
-            I.iC = 7 * I.M;
-            I.invM = 1.0f / float(I.M);
-            I.co = B.col_off[I.inst];
-            I.ro = B.row_off[I.inst];
-            I.rp = B.row_ptr + B.csr_off[I.inst];
-            I.Wd = B.row_ub[I.ro + I.m - 1];
-            I.W = int(I.Wd);
-            I.kc = B.c[I.co + I.iC];
-            solve_k1(B, Rz, cls, w, scol, sval, I, lane, hb_flag, launch_id);
+            const int64_t i = base + int64_t(bit) * S;
+            k1_instance(B, Rz, cls, w, scol, sval, lane, hb_flag, launch_id, i, B.n_cols[i], B.n_rows[i],
+                        B.col_off[i], B.row_off[i], B.csr_off[i]);
         }
     }
 }
