@@ -407,243 +407,7 @@ __global__ __launch_bounds__(64) void halda_lower_kernel(halda_model Mo, halda_f
 // per-wave global slice (kGlobal = true); want = 1 selects the flagged fleets only (gated on the
 // hand-back flag), want = 0 every fleet.
 
-// Device record of table entry g, compact: the five coefficients, the least-slack offsets of its
-// RAM / Metal row and of its VRAM rows, its class and GPU flag; W = L / k is set per k. dev()
-// expands it to exactly the Dev that decoding the lowered CSR gives (load_dev of decode_cap_row /
-// decode_cycle_row output), so the solve code is shared; bad = 1 where decode would reject.
-struct FieldRec {
-    double alpha, b, p_bp, p_b, cst;
-    int Kset, Kvram;  // kNoRow: the row is absent
-    int cls, gpu, W;
-    __device__ inline Dev dev() const {
-        Dev d;
-        d.cw = alpha; d.cn = b; d.cs0 = p_bp; d.cs1 = p_b; d.cs2 = p_bp; d.cs3 = cls == 2 ? p_b : p_bp;
-        // cycle rows: busy + z - C <= -cst, busy + F - z - C <= -cst (w entries alpha, alpha + b'/s_disk)
-        d.r1w = alpha;
-        d.r2w = alpha + p_bp;
-        d.rhs1 = -cst;
-        d.rhs2 = -cst;
-        d.wlo = 1; d.whi = W; d.nlo = 0; d.nhi = gpu ? W : 0;
-        const bool hs = Kset != kNoRow, hv = Kvram != kNoRow;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const bool mine = cls == j + 1;
-            d.slo[j] = 0;
-            d.shi[j] = mine ? W : 0;
-            d.us[j] = mine && hs ? 1 : 0;
-            d.vs[j] = j == 2 && mine && hs ? -1 : 0;
-            d.Ks[j] = mine ? Kset : kNoRow;
-        }
-        d.slo[3] = 0; d.shi[3] = gpu ? W : 0; d.us[3] = 0; d.vs[3] = hv ? 1 : 0; d.Ks[3] = Kvram;
-        // the link row n - w <= 0 (scale 1: K = floor(0 + 1e-9) = 0)
-        d.uf[0] = -1; d.vf[0] = 1; d.Kf[0] = 0;
-        d.uf[1] = 0; d.vf[1] = 0; d.Kf[1] = 0;
-        return d;
-    }
-    __device__ inline FieldRec shfl(int src) const {  // per-lane source (all lanes active)
-        FieldRec o;
-        o.alpha = shfl_f64(alpha, src); o.b = shfl_f64(b, src); o.p_bp = shfl_f64(p_bp, src);
-        o.p_b = shfl_f64(p_b, src); o.cst = shfl_f64(cst, src);
-        o.Kset = __shfl(Kset, src); o.Kvram = __shfl(Kvram, src);
-        const int cg = __shfl(cls | (gpu << 4), src);
-        o.cls = cg & 15; o.gpu = cg >> 4;
-        o.W = W;
-        return o;
-    }
-    template <class SG>
-    __device__ inline auto bcast(const SG &sg, int src) const;  // the problem's device src, on every lane
-    __device__ inline const FieldRec &core() const { return *this; }
-};
-
-// A record broadcast to the whole problem (every lane holds device src's record): its split takes
-// the branches on the record's shape instead of selects (they are uniform here), skipping the
-// candidates the device does not have; the same candidates, order and tie rule as on a FieldRec.
-struct UFieldRec : FieldRec {
-    __device__ inline const UFieldRec &core() const { return *this; }
-};
-
-template <class SG>
-__device__ inline auto FieldRec::bcast(const SG &sg, int src) const {
-    UFieldRec o;
-    o.alpha = sg.bcast(alpha, src); o.b = sg.bcast(b, src); o.p_bp = sg.bcast(p_bp, src);
-    o.p_b = sg.bcast(p_b, src); o.cst = sg.bcast(cst, src);
-    o.Kset = sg.bcast(Kset, src); o.Kvram = sg.bcast(Kvram, src);
-    const int cg = sg.bcast(cls | (gpu << 4), src);
-    o.cls = cg & 15; o.gpu = cg >> 4;
-    o.W = W;
-    return o;
-}
-
-// The solve primitives on a FieldRec, specialised. The Dev that dev() expands a record to has two
-// live slacks: its class slack s_c >= w + Kset (class 3: w - n + Kset; s_c <= W) and the VRAM slack
-// t >= n + Kvram (t <= nhi), both priced pv = (class 2 ? p_b : p_bp), with 0 <= n <= min(w, nhi),
-// nhi = W on a GPU device, else 0; every other slack is pinned to 0 by its bounds. So split_full /
-// split_step / dev_cycle below visit the same candidates with the same tie rule as on dev() and give
-// the same bits: a pinned slack adds p * 0 = +0, which leaves any sum of terms >= +0 unchanged, and
-// where that term is NaN there (an infinite price of another class: inf * 0) the cost is NaN here.
-__device__ inline double rec_pv(const FieldRec &r) { return r.cls == 2 ? r.p_b : r.p_bp; }
-__device__ inline bool rec_own(const FieldRec &r) { return unsigned(r.cls - 1) < 3u; }
-__device__ inline bool rec_nanx(const FieldRec &r) { return r.p_bp == kInf || (r.p_b == kInf && r.cls != 2); }
-__device__ inline int rec_wlo(const FieldRec &) { return 1; }
-__device__ inline int rec_whi(const FieldRec &r) { return r.W; }
-
-// Feasible n-interval for w layers (n_interval on dev()); false when no n is feasible (also when
-// the class 1 / 2 slack, which does not depend on n, exceeds its bound).
-__device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) {
-    const bool hs = r.Kset != kNoRow;
-    const int nhi = r.gpu ? r.W : 0;
-    nL = r.cls == 3 && hs ? max(0, w + r.Kset - r.W) : 0;
-    nU = min(nhi, w);
-    nU = r.Kvram != kNoRow ? min(nU, nhi - r.Kvram) : nU;
-    const bool setok = !(hs && (r.cls == 1 || r.cls == 2)) || max(0, w + r.Kset) <= r.W;
-    return nL <= nU && setok;
-}
-
-// One candidate n of a split, branch-free (selects, non-short-circuit tests): dev_cost on dev() for
-// (w, n) and its least slacks (sc = the class slack, t = VRAM), in dev_cost's term order (aw = alpha
-// w, pv = rec_pv, own = rec_own), and the tie rule "smaller cost, then smaller n". The record's NaN
-// flag (rec_nanx) is applied by the caller: it fails the whole split, as a NaN cost at every
-// candidate does.
-__device__ inline void rec_try(const FieldRec &r, double aw, double pv, bool own, int w, int nn, int nL, int nU,
-                               double &best, int &bn) {
-    nn = min(max(nn, nL), nU);
-    const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
-    double g = aw;
-    g = g + r.b * double(nn);
-    const double gs = g + pv * double(sc);
-    g = own ? gs : g;
-    g = g + pv * double(t);
-    const bool better = (g < best) | ((g == best) & (nn < bn));
-    best = better ? g : best;
-    bn = better ? nn : bn;
-}
-
-__device__ inline void rec_slacks(const FieldRec &r, int w, int n, int s[4]) {
-    const int sc = max(0, w - (r.cls == 3 ? n : 0) + r.Kset);
-    s[0] = r.cls == 1 ? sc : 0;
-    s[1] = r.cls == 2 ? sc : 0;
-    s[2] = r.cls == 3 ? sc : 0;
-    s[3] = max(0, n + r.Kvram);
-}
-
-// split_full on dev(): candidates nL, nU, the class-slack kink (class 3) and the VRAM kink, in that
-// order. Every candidate is evaluated on every lane (no divergent branches); an absent kink re-tries
-// nL, which never changes (best, bn): after nL's own try either bn = nL or best < cost(nL), and no
-// candidate lies below nL.
-template <bool kUniform>
-__device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int &n, int s[4]) {
-    int nL, nU;
-    const bool okI = rec_interval(r, w, nL, nU);
-    const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
-    double best = kInf;
-    int bn = -1;
-    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
-    const bool hc = r.cls == 3 && r.Kset != kNoRow, hv = r.Kvram != kNoRow;
-    if (!kUniform || hc) rec_try(r, aw, pv, own, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
-    if (!kUniform || hv) rec_try(r, aw, pv, own, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
-    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
-    if (ok) {
-        g = best;
-        n = bn;
-        rec_slacks(r, w, bn, s);
-    }
-    return ok;
-}
-__device__ inline bool split_full(const FieldRec &r, int w, double &g, int &n, int s[4]) {
-    return split_full_impl<false>(r, w, g, n, s);
-}
-// split_full at w = 1 (the record's lower bound): 0 <= nL <= n <= nU <= w = 1, so every kink clamps
-// to nL or nU and re-trying either is a no-op (after nU's try best <= cost(nU), and on a tie bn <= nU):
-// the two end tries give split_full's result.
-__device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, int s[4]) {
-    if (w != 1) return split_full(r, w, g, n, s);
-    int nL, nU;
-    const bool okI = rec_interval(r, w, nL, nU);
-    const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
-    double best = kInf;
-    int bn = -1;
-    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
-    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
-    if (ok) {
-        g = best;
-        n = bn;
-        rec_slacks(r, w, bn, s);
-    }
-    return ok;
-}
-// split_full at w = 2 (the greedy's first increment): 0 <= nL <= n <= nU <= 2, so the three tries
-// n = 0, 1, 2 (clamped to [nL, nU]) cover every candidate split_full tries (its kinks clamp into the
-// same range) with the same cost expression and tie rule: the same minimum and least minimiser, one
-// try fewer than split_full's four.
-__device__ inline bool split_second(const FieldRec &r, int w, double &g, int &n, int s[4]) {
-    if (w != 2) return split_full(r, w, g, n, s);
-    int nL, nU;
-    const bool okI = rec_interval(r, w, nL, nU);
-    const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
-    double best = kInf;
-    int bn = -1;
-    rec_try(r, aw, pv, own, w, 0, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, 1, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, 2, nL, nU, best, bn);
-    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
-    if (ok) {
-        g = best;
-        n = bn;
-        rec_slacks(r, w, bn, s);
-    }
-    return ok;
-}
-__device__ inline bool split_full(const UFieldRec &r, int w, double &g, int &n, int s[4]) {
-    return split_full_impl<true>(r, w, g, n, s);
-}
-
-__device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &g, int &n, int s[4]) {
-    int nL, nU;
-    const bool okI = rec_interval(r, w, nL, nU);
-    const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
-    double best = kInf;
-    int bn = -1;
-    rec_try(r, aw, pv, own, w, n_prev, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, n_prev + 1, nL, nU, best, bn);
-    const bool ok = okI & (bn >= 0) & !rec_nanx(r);
-    if (ok) {
-        g = best;
-        n = bn;
-        rec_slacks(r, w, bn, s);
-    }
-    return ok;
-}
-
-// dev_cycle on dev(): rows (alpha, alpha + p_bp) w + b n + slack terms <= -cst.
-__device__ inline void dev_cycle(const FieldRec &r, int w, int n, const int s[4], double &P, double &Q) {
-    const double pv = rec_pv(r);
-    const int sc = r.cls == 1 ? s[0] : r.cls == 2 ? s[1] : s[2];
-    const double t0 = r.b * double(n), tc = pv * double(sc), tv = pv * double(s[3]);
-    double a1 = r.alpha * double(w), a2 = (r.alpha + r.p_bp) * double(w);
-    a1 = a1 + t0; a2 = a2 + t0;
-    const bool own = rec_own(r);
-    const double o1 = a1 + tc, o2 = a2 + tc;
-    a1 = own ? o1 : a1;
-    a2 = own ? o2 : a2;
-    a1 = a1 + tv; a2 = a2 + tv;
-    const bool nanx = rec_nanx(r);
-    a1 = nanx ? __builtin_nan("") : a1;
-    a2 = nanx ? __builtin_nan("") : a2;
-    P = a1 - (-r.cst);
-    Q = a2 - (-r.cst);
-}
-
-__device__ inline double least_cycle(const FieldRec &r, int w, int n, const int s[4]) {
-    double P, Q;
-    dev_cycle(r, w, n, s, P, Q);
-    return Q >= P ? 0.5 * (P + Q) : P;
-}
+// FieldRec (the compact device record) and its specialised solve primitives: halda_solve.hpp.
 
 __device__ inline FieldRec field_rec(const SweepModel &Mo, const DevFields &F, int &bad) {
     FieldRec r;
