@@ -1452,8 +1452,7 @@ struct FleetsGroup : CtxHandle {
     StepsDesc *desc = nullptr;      // device copy of the plans' tables / results
     uint8_t *fflag = nullptr;       // k-slot form: per (plan, fleet) hand-back flags
     int *hb = nullptr;              // ... the launch's hand-back flag
-    unsigned *ctr = nullptr;        // ... the launch's item counter
-    int64_t lds = 0;                // ... the k-slot launch's LDS (the plan's + the next-item slot)
+    int64_t lds = 0;                // ... the k-slot launch's LDS (the plan's)
     unsigned grid = 0;
 };
 
@@ -1500,11 +1499,10 @@ int group_check(FleetsGroup *G) {
     int per_cu = 0;
     if (ksl) {
         const void *fn = reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel);
-        G->lds = align16(P0.p.lds) + 16;
+        G->lds = P0.p.lds;
         HIP_TRY(Ctx::ensure_lds(fn, G->lds));
         HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_tables_steps_kernel), P0.p.slice));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, int(P0.p.block1), size_t(G->lds)));
-        if (!G->ctr) HIP_TRY(hipMalloc(&G->ctr, 256));
         const size_t nfl = h.size() * size_t(P0.F.n_fleets);
         if (!G->fflag) HIP_TRY(hipMalloc(&G->fflag, std::max<size_t>(nfl, 1)));
         if (!G->hb) HIP_TRY(hipMalloc(&G->hb, sizeof(int)));
@@ -1541,7 +1539,6 @@ int halda_fleets_group_create(void *const *plans, int32_t n_plans, void **group,
         if (G->desc) (void)hipFree(G->desc);
         if (G->fflag) (void)hipFree(G->fflag);
         if (G->hb) (void)hipFree(G->hb);
-        if (G->ctr) (void)hipFree(G->ctr);
         delete G;
         return rc;
     }
@@ -1581,8 +1578,6 @@ int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *s
     SG.first = int(first % n);
     SG.steps = steps;
     SG.fflag = G->fflag;
-    SG.ctr = nullptr;
-    SG.next_off = 0;
     c->fleet_timed = false;
     c->have_lowered = false;
     const int nf = G->plans[0].F.n_fleets;
@@ -1594,15 +1589,12 @@ int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *s
         A.hb_flag = G->hb;
         A.launch_id = ++c->launch_id;
         A.want = 0;
-        const int64_t items = int64_t(steps) * ((nf + 64 / kSegLanes - 1) / (64 / kSegLanes));
-        if (items > (int64_t(1) << 31) - 1) return fail(HALDA_E_ARG, "halda_fleets_group_launch: too many items");
-        const unsigned grid = unsigned(std::min<int64_t>(G->grid, items));
-        SG.ctr = G->ctr;
-        SG.next_off = int(G->lds - 16);
-        HIP_TRY(hipMemsetAsync(G->ctr, 0, sizeof(unsigned), s));
+        if (steps > 65535) return fail(HALDA_E_ARG, "halda_fleets_group_launch: more than 65,535 k-slot steps");
+        // one workgroup per (batch, group of four fleets): the dispatcher's order is the items' order
+        const unsigned ng = unsigned((nf + 64 / kSegLanes - 1) / (64 / kSegLanes));
         HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel), G->lds));
-        hipLaunchKernelGGL(halda_sweep_kslot_steps_kernel, dim3(grid), dim3(p.block1), size_t(G->lds), s, A, p.SA,
-                           SG);
+        hipLaunchKernelGGL(halda_sweep_kslot_steps_kernel, dim3(ng, unsigned(steps)), dim3(p.block1), size_t(G->lds), s,
+                           A, p.SA, SG);
         HIP_TRY(hipGetLastError());
         if (c->timing) HIP_TRY(hipEventRecord(c->evfm, s));
         A.want = 1;  // the fleets flagged above, gated on the launch's hand-back flag
@@ -1639,7 +1631,6 @@ void halda_fleets_group_free(void *group) {
     if (G->desc) (void)hipFree(G->desc);
     if (G->fflag) (void)hipFree(G->fflag);
     if (G->hb) (void)hipFree(G->hb);
-    if (G->ctr) (void)hipFree(G->ctr);
     delete G;
 }
 

@@ -1095,8 +1095,6 @@ struct StepsArgs {
     int first;      // (first item's batch) mod n_desc
     int steps;
     uint8_t *fflag;  // k-slot steps: per (group entry, fleet) hand-back flags, n_desc x n_fleets
-    unsigned *ctr;   // ... the launch's item counter (zeroed before it)
-    int next_off;    // ... the LDS byte offset of the workgroup's next-item slot
 };
 
 __device__ inline const __attribute__((address_space(4))) StepsDesc &steps_desc(const StepsArgs &G, int b) {
@@ -1769,12 +1767,9 @@ __device__ inline int kslot_crit(const SlotArgs &SA) {
 
 // One k-slot workgroup's four fleets (group g: fleets 4 g .. 4 g + 3 of batch B), every slot wave: the
 // records (wave 0, shared through LDS), the tables, each slot's solve and the split scan's parts, the
-// pick. Three workgroup barriers on every wave's path; the LDS areas are written only after the first
-// of them, so a workgroup may run one group after another.
-// ctr / next (k-slot steps launch): wave 0 takes the workgroup's next item from the launch's counter at
-// the start and posts it in LDS before the last barrier, where every wave reads it after the group.
+// pick. Three workgroup barriers on every wave's path.
 __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepBatch &B, int64_t g,
-                            unsigned char *smem, int crit, unsigned *ctr = nullptr, int *next = nullptr) {
+                            unsigned char *smem, int crit) {
     constexpr int kPer = 64 / kSegLanes;
     const int lane = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // this wave's k-slot
@@ -1788,8 +1783,6 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
     if (q == crit) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);  // (a helper's raised priority ends with its group)
     SplitArea *split = reinterpret_cast<SplitArea *>(smem + SA.split_off) + seg;
-    unsigned nxt = 0;
-    if (ctr && q == 0 && lane == 0) nxt = atomicAdd(ctr, 1u);  // returns long before it is posted
     HALDA_KSTAMPW(0, __builtin_amdgcn_s_memtime());
     // slot 5: the constant-rate clock at start (low 40 bits), the wave's HW_ID[15:0] (SIMD, CU, SE) and
     // XCC_ID[3:0] above
@@ -1860,7 +1853,6 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         HALDA_KSTAMPW(10, t_rec[5]);
     }
     HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
-    if (ctr && q == 0 && lane == 0) *next = int(nxt);
     __syncthreads();
     HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
     if (q == 0 && f < nf) kslot_pick(A, B, SA, int(f), pick + seg * SA.n_slot, sg);
@@ -1872,36 +1864,24 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(Sweep
     kslot_group(A, SA, batch_of(A), int64_t(blockIdx.x), smem, kslot_crit(SA));
 }
 
-// halda_sweep_kslot_steps_kernel: `steps` batches of k-slot sweeps (C2 shapes) in one launch, the
-// group launch's k-slot form. Items (batch t, group of four fleets) in batch order, taken from a counter
-// one at a time by the resident workgroups, so a workgroup that ends a group early takes the next one at
-// once: the launch is paced by the mean group, not by the slowest of the 1,024 resident at once. Item
-// (t, gg) solves group g = (gg + t * kKslotRot) mod n_groups (a bijection per batch), which spreads a
-// slow group's batches over the launch. Fleets a slot flags go to the per-batch
-// flag array; halda_sweep_tables_steps_kernel redoes them after the launch.
+// halda_sweep_kslot_steps_kernel: `steps` batches of k-slot sweeps (C2 shapes) in one launch, the group
+// launch's k-slot form: one workgroup per item (batch t = blockIdx.y, group of four fleets), so the
+// hardware dispatcher hands the next item to whichever CU frees its resources first -- the launch is
+// paced by the mean group, not by the slowest of the 1,024 resident at once -- with the per-batch
+// kernel's registers (no item loop). Item (t, gg) solves group g = (gg + t * kKslotRot) mod n_groups (a
+// bijection per batch), which spreads a slow group's batches over the launch. Fleets a slot flags go to
+// the per-batch flag array; halda_sweep_tables_steps_kernel redoes them after the launch.
 constexpr int kKslotRot = 389;
 
 __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_steps_kernel(SweepArgs A, SlotArgs SA, StepsArgs G) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int crit = kslot_crit(SA);
     const int nf = A.F.n_fleets;
-    const int ng = (nf + 64 / kSegLanes - 1) / (64 / kSegLanes);
-    const int items = G.steps * ng;
-    // the next item: from the launch's counter (zeroed before the launch), so a workgroup that ends a
-    // group early takes the next one at once; the slot past the k-slot LDS areas carries it to the waves
-    int *next = reinterpret_cast<int *>(smem + G.next_off);
-    if (threadIdx.x == 0) *next = int(atomicAdd(G.ctr, 1u));
-    __syncthreads();
-    int i = *next;
-    while (i < items) {
-        const int t = i / ng, gg = i - t * ng;
-        const int g = int((int64_t(gg) + int64_t(t) * kKslotRot) % ng);
-        const int b = int((int64_t(G.first) + t) % G.n_desc);
-        const halda_fleets F = steps_fleets(steps_desc(G, b));
-        const FleetOut O = steps_out(steps_desc(G, b));
-        kslot_group(A, SA, SweepBatch{F, O, G.fflag + int64_t(b) * nf}, g, smem, crit, G.ctr, next);
-        i = *next;  // posted before the group's last barrier
-    }
+    const int ng = int(gridDim.x);
+    const int t = int(blockIdx.y), gg = int(blockIdx.x);
+    const int g = int((int64_t(gg) + int64_t(t) * kKslotRot) % ng);
+    const int b = int((int64_t(G.first) + t) % G.n_desc);
+    kslot_group(A, SA, SweepBatch{steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), G.fflag + int64_t(b) * nf},
+                g, smem, kslot_crit(SA));
 }
 
 // The gated table launch behind a k-slot steps launch: blockIdx.y = the group entry (first + y) mod

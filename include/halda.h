@@ -240,9 +240,9 @@ void halda_fleets_plan_free(void *plan);
  * steps) would leave them. When every plan is a register sweep of one shape (the same model, k list,
  * fleet count and fleet size uM <= 64, no x / c outputs: C3's resident copies) the steps run as ONE
  * launch whose resident waves take the (batch, fleet) items in batch order; when every plan is a k-slot
- * sweep of one shape (fleets of <= 16 devices with k > 1 tables: C2) as one k-slot launch whose
- * workgroups take the (batch, group of four fleets) items, then one gated table launch for the fleets
- * they flagged (*persistent = 1); otherwise batch by batch on `stream` (*persistent = 0). The group copies what it
+ * sweep of one shape (fleets of <= 16 devices with k > 1 tables: C2) as one k-slot launch of one
+ * workgroup per (batch, group of four fleets) item (steps <= 65,535), then one gated table launch for the
+ * fleets they flagged (*persistent = 1); otherwise batch by batch on `stream` (*persistent = 0). The group copies what it
  * needs from the plans at creation (the plans may be freed after it); the tables and result arrays
  * behind them must stay allocated while the group lives. Plans and groups fail with HALDA_E_ARG once
  * their context was freed. Replaces the per-batch loop over halda_solve (halda_p_solver.py:369-436)
