@@ -790,7 +790,7 @@ def main():
 
     def sweep_group(k):
         # the headline: K batches (copy (turn + t) % n_sw each) in ONE launch on one stream
-        # (halda_fleets_group_launch: resident waves prefetch each next (fleet, batch)'s fields)
+        # (halda_fleets_group_launch: one wave per (batch, fleet) item)
         group.launch(turn[0], k, sref)
         turn[0] += k
 
@@ -953,8 +953,8 @@ def main():
             },
             "launch": {"what": "the K steps as ONE group launch (halda_fleets_group_launch -> "
                                "halda_sweep_steps_kernel): batch t reads resident copy (first + t) % copies and writes "
-                               "its results, bit-identical to its own launch; resident waves load each next (fleet, "
-                               "batch)'s fields while solving the current one",
+                               "its results, bit-identical to its own launch; one wave per (batch, fleet) item, the "
+                               "hardware dispatcher starting the next batch's waves where the last ones end",
                        "persistent": group.persistent, "launches_per_region": 1 if group.persistent else args.steps,
                        "stream": 1},
             "per_launch": {"what": "the same K steps as K launches (one per batch, halda_fleets_plan_launch_many) "

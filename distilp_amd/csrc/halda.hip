@@ -1453,7 +1453,6 @@ struct FleetsGroup : CtxHandle {
     uint8_t *fflag = nullptr;       // k-slot form: per (plan, fleet) hand-back flags
     int *hb = nullptr;              // ... the launch's hand-back flag
     int64_t lds = 0;                // ... the k-slot launch's LDS (the plan's)
-    unsigned grid = 0;
 };
 
 bool same_model(const halda_model &a, const halda_model &b) { return std::memcmp(&a, &b, sizeof a) == 0; }
@@ -1494,25 +1493,16 @@ int group_check(FleetsGroup *G) {
     HIP_TRY(hipMemcpy(G->desc, h.data(), sizeof(StepsDesc) * h.size(), hipMemcpyHostToDevice));
     G->A = P0.p.A;
     G->kslot = ksl;
-    // every workgroup resident at once: the occupancy of the steps kernel on every CU (the launch caps it
-    // at one workgroup per item)
-    int per_cu = 0;
     if (ksl) {
-        const void *fn = reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel);
         G->lds = P0.p.lds;
-        HIP_TRY(Ctx::ensure_lds(fn, G->lds));
+        HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel), G->lds));
         HIP_TRY(Ctx::ensure_lds(reinterpret_cast<const void *>(halda_sweep_tables_steps_kernel), P0.p.slice));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, int(P0.p.block1), size_t(G->lds)));
         const size_t nfl = h.size() * size_t(P0.F.n_fleets);
         if (!G->fflag) HIP_TRY(hipMalloc(&G->fflag, std::max<size_t>(nfl, 1)));
         if (!G->hb) HIP_TRY(hipMalloc(&G->hb, sizeof(int)));
         HIP_TRY(hipMemset(G->fflag, 0, std::max<size_t>(nfl, 1)));
         HIP_TRY(hipMemset(G->hb, 0, sizeof(int)));
-    } else {
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void *>(halda_sweep_steps_kernel), 64 * kSweepWavesPerBlock, 0));
     }
-    G->grid = unsigned(std::max(per_cu, 1) * c->cus);
     G->persistent = true;
     return HALDA_OK;
 }
@@ -1603,10 +1593,11 @@ int halda_fleets_group_launch(void *group, int64_t first, int32_t steps, void *s
                            dim3(64), size_t(p.slice), s, A, SG);
         HIP_TRY(hipGetLastError());
     } else {
-        const int64_t items = int64_t(steps) * nf;
-        const unsigned grid =
-            unsigned(std::min<int64_t>(G->grid, (items + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock));
-        hipLaunchKernelGGL(halda_sweep_steps_kernel, dim3(grid), dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
+        // one wave per (batch, fleet) item: grid (fleet blocks, steps)
+        if (steps > 65535) return fail(HALDA_E_ARG, "halda_fleets_group_launch: more than 65,535 steps");
+        hipLaunchKernelGGL(halda_sweep_steps_kernel,
+                           dim3(unsigned((nf + kSweepWavesPerBlock - 1) / kSweepWavesPerBlock), unsigned(steps)),
+                           dim3(64 * kSweepWavesPerBlock), 0, s, G->A, SG);
         HIP_TRY(hipGetLastError());
     }
     if (c->timing) {

@@ -655,8 +655,8 @@ __device__ inline void flag_fleet(const SweepArgs &A, int f, int lane) { flag_fl
 // tables in the segment's LDS slice, k = 1 register greedy and k > 1 incremental threshold scan
 // only: what that cannot do (fast-path fallbacks, non-convex / non-monotone leaves) is flagged for
 // the one-fleet-per-wave table launch, as the register-only launch does.
-// The steps kernel's prefetched fleet: the fields of the lane's device (loaded while the wave solved the
-// previous fleet), the fleet's first device, and the lane's k_j / W_j (loaded once per wave).
+// A fleet handed to sweep_fleet with its fields already loaded (the steps kernel, the resident wave): the
+// fields of the lane's device, the fleet's first device, and the lane's k_j / W_j.
 struct SweepPre {
     DevFields mf;
     int64_t d0;
@@ -1120,50 +1120,36 @@ __device__ inline FleetOut steps_out(const __attribute__((address_space(4))) Ste
     return o;
 }
 
+// halda_sweep_steps_kernel: the group launch's register form -- `steps` batches of register sweeps in ONE
+// launch, one wave per (batch, fleet) item (grid = fleet blocks x steps, blockIdx.y the batch). The
+// hardware dispatcher starts each next item's wave on whichever SIMD a wave just left, so one batch's
+// tail overlaps the next batch's start, and a wave holds no loop state: 67 VGPRs, seven waves per SIMD
+// (the resident-wave form with an item loop: 79 VGPRs, six per SIMD, 49 SGPR spills, 12 % slower).
+// Every item runs the same sweep_fleet as halda_sweep_kernel on the same fields (kPre: the fields handed
+// in; kXC = false: no x / c), so each batch's results are bit-identical to its own launch.
 #ifndef HALDA_STEPS_WAVES
-#define HALDA_STEPS_WAVES 6  // resident waves per SIMD of the steps kernel
+#define HALDA_STEPS_WAVES 6  // occupancy floor of the steps kernel (it takes seven at 67 VGPRs)
 #endif
 
-__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void halda_sweep_steps_kernel(
-    SweepArgs A, StepsArgs G) {
-    const int gw = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
-    const int nw = int(gridDim.x) * kSweepWavesPerBlock;
+__global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void halda_sweep_steps_kernel(SweepArgs A,
+                                                                                                   StepsArgs G) {
+    const int f = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * kSweepWavesPerBlock + int(threadIdx.x >> 6));
     const int lane = int(threadIdx.x & 63);
     const int nf = A.F.n_fleets, M = A.uM;
-    if (G.steps <= 0 || nf <= 0) return;
-    // items in batch order, item i = (batch t = i / nf, fleet f = i % nf); wave g takes g, g + nw, ...
-    int f = gw % nf, t = gw / nf;
-    if (t >= G.steps) return;
-    int b = int((int64_t(G.first) + t) % G.n_desc);
-    const int dt = nw / nf, df = nw % nf, db = dt % G.n_desc;
+    if (f >= nf) return;
+    const int b = int((int64_t(G.first) + blockIdx.y) % G.n_desc);
     __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
     const Wave wv(lane);
     SweepPre cur;
-    {
-        const bool kl = lane < A.n_k;
-        cur.kj = A.ks[kl ? lane : 0];
-        cur.Wj = kl ? A.Ws[lane] : 0;
-    }
-    const int dl = lane < M ? lane : 0;
-    while (true) {
-        cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
-        cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + dl);
-        sweep_fleet<false, false, Wave, true>(A, steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), f, w,
-                                              wv, &cur);
-        // the wave's next item, nw items on
-        f += df;
-        t += dt;
-        b += db;
-        if (f >= nf) {
-            f -= nf;
-            ++t;
-            ++b;
-        }
-        if (b >= G.n_desc) b -= G.n_desc;
-        if (t >= G.steps) break;
-    }
+    const bool kl = lane < A.n_k;
+    cur.kj = A.ks[kl ? lane : 0];
+    cur.Wj = kl ? A.Ws[lane] : 0;
+    cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
+    cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + (lane < M ? lane : 0));
+    sweep_fleet<false, false, Wave, true>(A, steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), f, w, wv,
+                                          &cur);
 }
 
 // ---------------------------------------------------------------- resident single-fleet solver

@@ -239,7 +239,7 @@ void halda_fleets_plan_free(void *plan);
  * its own plan's arrays, exactly as halda_fleets_plan_launch_many(plans, n_plans, &stream, 1, first,
  * steps) would leave them. When every plan is a register sweep of one shape (the same model, k list,
  * fleet count and fleet size uM <= 64, no x / c outputs: C3's resident copies) the steps run as ONE
- * launch whose resident waves take the (batch, fleet) items in batch order; when every plan is a k-slot
+ * launch of one wave per (batch, fleet) item (steps <= 65,535); when every plan is a k-slot
  * sweep of one shape (fleets of <= 16 devices with k > 1 tables: C2) as one k-slot launch of one
  * workgroup per (batch, group of four fleets) item (steps <= 65,535), then one gated table launch for the
  * fleets they flagged (*persistent = 1); otherwise batch by batch on `stream` (*persistent = 0). The group copies what it

@@ -43,10 +43,11 @@ def _check(dt, want, per_k):
 @pytest.mark.parametrize("nf,n_tab,first,steps,per_k", [(300, 3, 2, 7, True), (4096 + 77, 4, 5, 13, False),
                                                          (64, 5, 0, 20, False), (1, 2, 1, 3, True)])
 def test_group_launch_equals_per_table_solves(llama_online_model, nf, n_tab, first, steps, per_k):
-    """C3-shaped tables (M = 64, every k of L = 80): the group runs as ONE persistent launch; every batch
-    (table (first + t) % n_tab) leaves the bits of its own synchronous solve -- fewer fleets than
-    resident waves, more (waves taking two fleets), a batch count that is not a multiple of the tables
-    and one fleet alone. The outputs are zeroed first, so every table must be written by the launch."""
+    """C3-shaped tables (M = 64, every k of L = 80): the group runs as ONE launch (one wave per (batch,
+    fleet) item); every batch (table (first + t) % n_tab) leaves the bits of its own synchronous solve --
+    a fleet count that is not a multiple of the four-wave workgroups, 4,173 fleets, a batch count that is
+    not a multiple of the tables and one fleet alone. The outputs are zeroed first, so every table must be
+    written by the launch."""
     import torch
 
     from distilp_amd.solver.fleets import DeviceFleetTable, PlanGroup
