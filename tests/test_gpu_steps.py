@@ -66,6 +66,8 @@ def test_group_launch_equals_per_table_solves(llama_online_model, nf, n_tab, fir
             v.zero_()
     stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize(dev)
+    with pytest.raises(RuntimeError):  # one launch carries at most 65,535 batches (the grid's y extent)
+        group.launch(first, 65536, stream.cuda_stream)
     group.launch(first, steps, stream.cuda_stream)
     torch.cuda.synchronize(dev)
     for t in range(n_tab):
