@@ -500,11 +500,11 @@ def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
     instances through halda_solve_fleets_host (PCIe in, the k-sweep, PCIe out), one at a time."""
     from dataclasses import replace
 
-    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, solve_table
+    from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS, fleet_table, solve_table
 
     base = fleet_table(build_fleets([0], M), model)
     big = replace(base, dev_off=np.arange(B + 1, dtype=np.int64) * M,
-                  **{f: np.tile(getattr(base, f), B) for f in ("os_class", "flags") + F64_FIELDS + I64_FIELDS})
+                  **{f: np.tile(getattr(base, f), B) for f in ("os_class", "flags") + F64_FIELDS + BYTE_FIELDS})
     rng = np.random.default_rng(10_000)
     solve_table(big.perturbed(rng), model, KS_L80, 0.5)  # warm-up
     t0 = time.perf_counter()

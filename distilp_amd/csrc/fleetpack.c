@@ -6,10 +6,11 @@
  * the reference's truthiness tests, see fleets.py), so the single-fleet halda_solve path spends
  * microseconds, not a Python loop, before the GPU call.
  *
- *   pack(fleets, Q, fq, fout, f64, i64, u8, off, heads) -> None
+ *   pack(fleets, Q, fq, fout, f64, b64, u8, off, heads) -> None
  *     fleets  sequence of sequences of DeviceProfile
  *     Q       the model's quantisation key; fq / fout: "b_1" in model.f_q / model.f_out
- *     f64     writable float64 buffer [10][nd] (F64_FIELDS rows), i64: int64 [6][nd], u8: uint8
+ *     f64     writable float64 buffer [10][nd] (F64_FIELDS rows), b64: float64 [6][nd] (BYTE_FIELDS rows: the
+ *             integer byte counts as doubles, exact below 2^53), u8: uint8
  *     [2][nd] (os_class row, flags row), off: int64 [n_fleets + 1], heads: int64 [n_fleets]
  *   raises what fleets.fleet_table_py raises, FleetTable.check's ZeroDivisionErrors included
  */
@@ -111,7 +112,7 @@ typedef struct {
     Py_hash_t hQ;
     int fq;
     double *f64;
-    int64_t *i64;
+    double *b64;
     uint8_t *cls, *flg;
     volatile int *bail;
 } Job;
@@ -228,7 +229,7 @@ static int fast_dev(const Job *J, PyObject *d, Py_ssize_t g) {
     }
     const Py_ssize_t nd = J->nd;
     for (int a = 0; a < 10; ++a) J->f64[a * nd + g] = fv[a];
-    for (int a = 0; a < 6; ++a) J->i64[a * nd + g] = iv[a];
+    for (int a = 0; a < 6; ++a) J->b64[a * nd + g] = (double)iv[a];
     J->cls[g] = (uint8_t)c;
     J->flg[g] = (uint8_t)fl;
     return 0;
@@ -278,7 +279,7 @@ static int pack_threads(Py_ssize_t nd) {
 }
 
 /* 1: packed in parallel; 0: not attempted / given up (the caller packs serially); -1: error set */
-static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f64, int64_t *i64, uint8_t *cls,
+static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f64, double *b64, uint8_t *cls,
                          int64_t *off, int64_t *heads, Py_ssize_t nd) {
     (void)fout;
     const Py_ssize_t nf = PySequence_Fast_GET_SIZE(seq);
@@ -316,11 +317,11 @@ static int pack_parallel(PyObject *seq, PyObject *Q, int fq, int fout, double *f
     volatile int bail = 0;
     int started = 0;
     if (nt == 1) { /* small tables: the same read-only pass on the calling thread */
-        jobs[0] = (Job){devs, 0, nd, nd, Q, hQ, fq, f64, i64, cls, cls + nd, &bail};
+        jobs[0] = (Job){devs, 0, nd, nd, Q, hQ, fq, f64, b64, cls, cls + nd, &bail};
         worker(&jobs[0]);
     }
     for (int t = 0; t < nt && nt > 1; ++t) {
-        jobs[t] = (Job){devs, nd * t / nt, nd * (t + 1) / nt, nd, Q, hQ, fq, f64, i64, cls, cls + nd, &bail};
+        jobs[t] = (Job){devs, nd * t / nt, nd * (t + 1) / nt, nd, Q, hQ, fq, f64, b64, cls, cls + nd, &bail};
         if (pthread_create(&th[t], NULL, worker, &jobs[t]) != 0) { bail = 1; break; }
         ++started;
     }
@@ -351,11 +352,12 @@ static PyObject *pack(PyObject *self, PyObject *args) {
         goto done;
     }
     double *f64 = (double *)bf.buf;
-    int64_t *i64 = (int64_t *)bi.buf, *off = (int64_t *)bo.buf, *heads = (int64_t *)bh.buf;
+    double *b64 = (double *)bi.buf;
+    int64_t *off = (int64_t *)bo.buf, *heads = (int64_t *)bh.buf;
     uint8_t *cls = (uint8_t *)bu.buf, *flg = cls + nd;
     Py_ssize_t g = 0;
     {
-        const int par = pack_parallel(seq, Q, fq, fout, f64, i64, cls, off, heads, nd);
+        const int par = pack_parallel(seq, Q, fq, fout, f64, b64, cls, off, heads, nd);
         if (par < 0) goto done;
         if (par == 1) {
             g = nd;
@@ -480,7 +482,7 @@ static PyObject *pack(PyObject *self, PyObject *args) {
                 }
                 if (PyErr_Occurred()) break;
                 for (int a = 0; a < 10; ++a) f64[a * nd + g] = fv[a];
-                for (int a = 0; a < 6; ++a) i64[a * nd + g] = iv[a];
+                for (int a = 0; a < 6; ++a) b64[a * nd + g] = (double)iv[a];
                 cls[g] = (uint8_t)c;
                 flg[g] = (uint8_t)fl;
                 err = 0;
@@ -522,7 +524,7 @@ done:
     return ret;
 }
 
-/* consts(f64, i64, u8, off, heads, fout, f_out_b1, b_in, b_out, V, out) -> None
+/* consts(f64, b64, u8, off, heads, fout, f_out_b1, b_in, b_out, V, out) -> None
  * Per fleet of a packed table, the constant part of obj_value in the reference's own order
  * (halda_p_solver.py:356-357, dense_common.py:211-230): out[0][f] = sum t_comm and out[1][f] = sum xi
  * over the devices from the first (Python's `s = 0; for d in devs: s += ...`), out[2][f] = kappa: the
@@ -544,11 +546,12 @@ static PyObject *consts(PyObject *self, PyObject *args) {
     }
     {
         const double *f64 = (const double *)bf.buf;
-        const int64_t *i64 = (const int64_t *)bi.buf, *off = (const int64_t *)bo.buf, *heads = (const int64_t *)bh.buf;
+        const double *b64 = (const double *)bi.buf;
+        const int64_t *off = (const int64_t *)bo.buf, *heads = (const int64_t *)bh.buf;
         const uint8_t *cls = (const uint8_t *)bu.buf, *flg = cls + nd;
         const double *scpu = f64, *Tc = f64 + 2 * nd, *r2v = f64 + 6 * nd, *v2r = f64 + 7 * nd, *tcomm = f64 + 8 * nd,
                      *sd = f64 + 9 * nd;
-        const int64_t *ram = i64, *ccpu = i64 + nd, *swap = i64 + 5 * nd;
+        const double *ram = b64, *ccpu = b64 + nd, *swap = b64 + 5 * nd;
         double *out = (double *)bout.buf;
         for (Py_ssize_t f = 0; f < nf; ++f) {
             const int64_t a = off[f], b = off[f + 1], h = heads[f];
@@ -567,7 +570,7 @@ static PyObject *consts(PyObject *self, PyObject *args) {
             double tail = 0.0;
             for (int pass = 1; pass <= 3; pass += 2)
                 for (int64_t j = a; j < b; ++j)
-                    if (cls[j] == pass) tail += (double)(ccpu[j] - ram[j] - swap[j]) / sd[j];
+                    if (cls[j] == pass) tail += ((ccpu[j] - ram[j]) - swap[j]) / sd[j];
             out[f] = t;
             out[nf + f] = x;
             out[2 * nf + f] = total + tail;

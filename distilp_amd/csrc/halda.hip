@@ -1690,14 +1690,14 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     HIP_TRY(up(o_fl, fh->flags, nd));
     const double *f64[10] = {fh->scpu_b1, fh->sgpu_b1, fh->T_cpu, fh->T_gpu, fh->t_kvcpy_cpu,
                              fh->t_kvcpy_gpu, fh->t_ram2vram, fh->t_vram2ram, fh->t_comm, fh->s_disk};
-    const int64_t *i64[6] = {fh->d_avail_ram, fh->c_cpu, fh->c_gpu, fh->d_avail_cuda, fh->d_avail_metal, fh->swap};
+    const double *b64[6] = {fh->d_avail_ram, fh->c_cpu, fh->c_gpu, fh->d_avail_cuda, fh->d_avail_metal, fh->swap};
     for (int a = 0; a < 10; ++a) {
         if (!f64[a] || !fh->os_class || !fh->flags) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
         HIP_TRY(up(o_f64 + 8 * nd * a, f64[a], 8 * nd));
     }
     for (int a = 0; a < 6; ++a) {
-        if (!i64[a]) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
-        HIP_TRY(up(o_i64 + 8 * nd * a, i64[a], 8 * nd));
+        if (!b64[a]) return fail(HALDA_E_ARG, "halda_fleets has a NULL array");
+        HIP_TRY(up(o_i64 + 8 * nd * a, b64[a], 8 * nd));
     }
     // small calls (a single halda_solve: ~8 KB in, ~70 KB out) skip both copies: the kernels read the
     // table from and write the results to the pinned buffer itself, across PCIe, and the host polls
@@ -1711,7 +1711,7 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
         HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));  // the table (and x_off)
     }
     auto F64 = [&](int a) { return reinterpret_cast<const double *>(base + o_f64 + 8 * nd * a); };
-    auto I64 = [&](int a) { return reinterpret_cast<const int64_t *>(base + o_i64 + 8 * nd * a); };
+    auto I64 = [&](int a) { return reinterpret_cast<const double *>(base + o_i64 + 8 * nd * a); };
     d.dev_off = reinterpret_cast<const int64_t *>(base + o_doff);
     d.os_class = reinterpret_cast<const uint8_t *>(base + o_cls);
     d.flags = reinterpret_cast<const uint8_t *>(base + o_fl);

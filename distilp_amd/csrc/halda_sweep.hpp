@@ -56,7 +56,8 @@ struct DevCoef {
 // trip for all of them), the coefficients computed from the registers.
 struct DevFields {
     double scpu, sgpu, Tc, Tg, tkc, tkg, r2v, v2r, tcomm, sdisk;
-    int64_t ram, ccpu, cgpu, cuda, metal, swap;
+    double ram, ccpu, cgpu, cuda, metal, swap;  // byte counts: integers below 2^53, so the integer sums and
+                                                // differences of the reference are exact in double
     int cls, flags;
 };
 
@@ -96,7 +97,7 @@ __device__ inline DevCoef dev_coef(const halda_model &Mo, const DevFields &F, do
     o.b = cls == 1 ? 0.0 : beta;
     o.xi = (F.r2v + F.v2r) * ((fl & HALDA_DEV_UMA) ? 0.0 : 1.0);
     const double head = (fl & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-    o.bcio = bvo * head + double(F.ccpu);
+    o.bcio = bvo * head + F.ccpu;
     const double sd = fmax(1.0, F.sdisk);
     o.p_bp = bp / sd;
     o.p_b = Mo.b_layer / sd;
@@ -113,14 +114,14 @@ __device__ inline DevCoef dev_coef(const halda_model &Mo, const halda_fleets &F,
 
 // Right-hand sides of the capacity rows (halda_p_solver.py:227-277).
 __device__ inline double rhs_ram(const DevFields &F, int set, double bcio) {
-    if (set == 1) return double(F.ram) - bcio;
-    if (set == 2) return double(F.metal) - bcio - double(F.cgpu);
-    return double(F.ram + F.swap) - bcio;
+    if (set == 1) return F.ram - bcio;
+    if (set == 2) return F.metal - bcio - F.cgpu;
+    return (F.ram + F.swap) - bcio;  // the reference's integer sum, exact
 }
-__device__ inline double rhs_cuda(const DevFields &F) { return double(F.cuda) - double(F.cgpu); }
+__device__ inline double rhs_cuda(const DevFields &F) { return F.cuda - F.cgpu; }
 __device__ inline double rhs_metal(const halda_model &Mo, const DevFields &F) {
     const double head = (F.flags & HALDA_DEV_HEAD) ? 1.0 : 0.0;
-    return double(F.metal) - double(F.cgpu) - Mo.b_out * head;
+    return F.metal - F.cgpu - Mo.b_out * head;
 }
 __device__ inline double rhs_ram(const halda_fleets &F, int64_t g, int set, double bcio) {
     return rhs_ram(load_fields(F, g), set, bcio);
@@ -145,7 +146,7 @@ __device__ inline void fleet_offsets(const halda_model &Mo, const halda_fleets &
         const double tc = F.t_comm[g];
         const double xv = (F.t_ram2vram[g] + F.t_vram2ram[g]) * ((F.flags[g] & HALDA_DEV_UMA) ? 0.0 : 1.0);
         const int cls = F.os_class[g];
-        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const double tl = ((F.c_cpu[g] - F.d_avail_ram[g]) - F.swap[g]) / F.s_disk[g];
         const uint64_t heads = __ballot(i0 + lane < M && (F.flags[g] & HALDA_DEV_HEAD));
         if (hi < 0 && heads) hi = i0 + __builtin_ctzll(heads);
         const int n = min(64, M - i0);
@@ -161,7 +162,7 @@ __device__ inline void fleet_offsets(const halda_model &Mo, const halda_fleets &
         const int i = min(i0 + lane, M - 1);
         const int64_t g = d0 + i;
         const int cls = F.os_class[g];
-        const double tl = double(F.c_cpu[g] - F.d_avail_ram[g] - F.swap[g]) / F.s_disk[g];
+        const double tl = ((F.c_cpu[g] - F.d_avail_ram[g]) - F.swap[g]) / F.s_disk[g];
         const int n = min(64, M - i0);
         for (int q = 0; q < n; ++q)
             if (bcast(cls, q) == 3) tail += bcast(tl, q);
@@ -473,7 +474,7 @@ struct FieldSrc {
 // reductions): sum t_comm, sum xi, kappa with the head's terms (dense_common.py:211-230). For
 // M <= 64 lane i passes device i's fields (in registers) and the head's come by readlane.
 __device__ inline double tail_term(const DevFields &f) {
-    return f.cls != 2 ? double(f.ccpu - f.ram - f.swap) / f.sdisk : 0.0;
+    return f.cls != 2 ? ((f.ccpu - f.ram) - f.swap) / f.sdisk : 0.0;
 }
 __device__ inline double xi_term(const DevFields &f) { return (f.r2v + f.v2r) * ((f.flags & HALDA_DEV_UMA) ? 0.0 : 1.0); }
 

@@ -18,7 +18,7 @@ import numpy as np
 
 LIB_PATH = Path(os.environ.get("HALDA_LIB", Path(__file__).resolve().parent.parent / "libhalda.so"))
 
-ABI_VERSION = 2  # include/halda.h HALDA_ABI_VERSION (2: halda_fleet_result.x_off)
+ABI_VERSION = 3  # include/halda.h HALDA_ABI_VERSION (2: halda_fleet_result.x_off; 3: byte counts as double)
 
 STATUS_OPTIMAL = 0
 STATUS_LIMIT = 1

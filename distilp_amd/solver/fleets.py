@@ -41,7 +41,9 @@ DEV_HEAD, DEV_UMA, DEV_CPU_RATE, DEV_GPU, DEV_GPU_RATE, DEV_CUDA_OK, DEV_METAL_O
 
 F64_FIELDS = ("scpu_b1", "sgpu_b1", "T_cpu", "T_gpu", "t_kvcpy_cpu", "t_kvcpy_gpu", "t_ram2vram", "t_vram2ram",
               "t_comm", "s_disk")
-I64_FIELDS = ("d_avail_ram", "c_cpu", "c_gpu", "d_avail_cuda", "d_avail_metal", "swap")
+# the profiles' integer byte counts, held as float64 (ABI 3): exact below 2^53, so the reference's integer
+# sums and differences of them are exact in the kernels' double arithmetic
+BYTE_FIELDS = ("d_avail_ram", "c_cpu", "c_gpu", "d_avail_cuda", "d_avail_metal", "swap")
 
 
 class HaldaModelC(ctypes.Structure):
@@ -53,7 +55,7 @@ class HaldaModelC(ctypes.Structure):
 class HaldaFleetsC(ctypes.Structure):
     _fields_ = ([("n_fleets", ctypes.c_int32), ("min_devices", ctypes.c_int32), ("max_devices", ctypes.c_int32),
                  ("dev_off", ctypes.c_void_p), ("os_class", ctypes.c_void_p), ("flags", ctypes.c_void_p)]
-                + [(f, ctypes.c_void_p) for f in F64_FIELDS] + [(f, ctypes.c_void_p) for f in I64_FIELDS])
+                + [(f, ctypes.c_void_p) for f in F64_FIELDS] + [(f, ctypes.c_void_p) for f in BYTE_FIELDS])
 
 
 class HaldaFleetResultC(ctypes.Structure):
@@ -147,7 +149,7 @@ class FleetTable:
     t_vram2ram: np.ndarray
     t_comm: np.ndarray
     s_disk: np.ndarray
-    d_avail_ram: np.ndarray  # int64
+    d_avail_ram: np.ndarray  # float64 (integer byte counts, BYTE_FIELDS)
     c_cpu: np.ndarray
     c_gpu: np.ndarray
     d_avail_cuda: np.ndarray
@@ -187,7 +189,7 @@ class FleetTable:
             return np.exp(rng.uniform(np.log(lo), np.log(hi), n))
 
         upd = {f: getattr(self, f) * lu() for f in F64_FIELDS}
-        upd.update({f: np.floor(getattr(self, f) * lu()).astype(np.int64) for f in I64_FIELDS})
+        upd.update({f: np.floor(getattr(self, f) * lu()) for f in BYTE_FIELDS})  # still integers
         return replace(self, **upd)
 
     def check(self, heads: Optional[np.ndarray] = None) -> None:
@@ -241,20 +243,20 @@ def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) 
     nf = len(fleets)
     nd = sum(len(d) for d in fleets)
     f64 = np.empty((len(F64_FIELDS), nd), np.float64)
-    i64 = np.empty((len(I64_FIELDS), nd), np.int64)
+    b64 = np.empty((len(BYTE_FIELDS), nd), np.float64)
     u8 = np.empty((2, nd), np.uint8)
     off = np.empty(nf + 1, np.int64)
     heads = np.empty(nf, np.int64)
-    _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, i64, u8, off, heads)
+    _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, b64, u8, off, heads)
     # the dataclass's fields set directly (no per-field __setattr__), then the packed blocks they view
     t = object.__new__(FleetTable)
     d = t.__dict__
     d["dev_off"], d["os_class"], d["flags"] = off, u8[0], u8[1]
     for j, f in enumerate(F64_FIELDS):
         d[f] = f64[j]
-    for j, f in enumerate(I64_FIELDS):
-        d[f] = i64[j]
-    d["_blocks"] = (off, u8, f64, i64)  # FleetTable.check ran in the packer
+    for j, f in enumerate(BYTE_FIELDS):
+        d[f] = b64[j]
+    d["_blocks"] = (off, u8, f64, b64)  # FleetTable.check ran in the packer
     d["_heads"] = heads                  # kappa's head of each fleet (global device index)
     return t
 
@@ -311,11 +313,11 @@ def fleet_table_py(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfil
                         min(g["d_bytes_can_swap"], g["d_swap_avail"]) if os_type == "android" else 0))
         off.append(off[-1] + len(devs))
     fa = np.array(f64, dtype=np.float64).reshape(-1, len(F64_FIELDS))
-    ia = np.array(i64, dtype=np.int64).reshape(-1, len(I64_FIELDS))
+    ia = np.array(i64, dtype=np.int64).reshape(-1, len(BYTE_FIELDS)).astype(np.float64)  # as the C packer
     t = FleetTable(dev_off=np.asarray(off, np.int64), os_class=np.asarray(cls, np.uint8),
                    flags=np.asarray(flags, np.uint8),
                    **{f: np.ascontiguousarray(fa[:, j]) for j, f in enumerate(F64_FIELDS)},
-                   **{f: np.ascontiguousarray(ia[:, j]) for j, f in enumerate(I64_FIELDS)})
+                   **{f: np.ascontiguousarray(ia[:, j]) for j, f in enumerate(BYTE_FIELDS)})
     t.check(np.asarray(heads, np.int64))
     return t
 
@@ -340,10 +342,10 @@ def fleet_constants(table: "FleetTable", model: ModelProfile):
     blocks, heads = getattr(table, "_blocks", None), getattr(table, "_heads", None)
     if _PACKER is None or blocks is None or heads is None or not hasattr(_PACKER, "consts"):
         return fleet_constants_np(table, model)
-    off, u8, f64, i64 = blocks
+    off, u8, f64, b64 = blocks
     out = np.empty((3, table.n_fleets))
     fout = "b_1" in model.f_out
-    _PACKER.consts(f64, i64, u8, off, heads, fout, float(model.f_out["b_1"]) if fout else 0.0, float(model.b_in),
+    _PACKER.consts(f64, b64, u8, off, heads, fout, float(model.f_out["b_1"]) if fout else 0.0, float(model.b_in),
                    float(model.b_out), float(model.V), out)
     return out[0], out[1], out[2]
 
@@ -383,7 +385,7 @@ def fleet_constants_np(table: "FleetTable", model: ModelProfile):
     cls = _padded(table, table.os_class.astype(np.int64), fill=0)
     rank = np.where(cls == 1, 0, np.where(cls == 3, 1, 2))
     order = np.argsort(rank * (cls.shape[1] + 1) + np.arange(cls.shape[1])[None, :], axis=1, kind="stable")
-    term = (table.c_cpu - table.d_avail_ram - table.swap).astype(np.float64) / table.s_disk
+    term = ((table.c_cpu - table.d_avail_ram) - table.swap) / table.s_disk  # integer byte counts: exact
     tm = np.take_along_axis(np.where(rank < 2, _padded(table, term), 0.0), order, axis=1)
     tail = np.zeros(nf)
     for i in range(tm.shape[1]):
@@ -423,7 +425,7 @@ def _fleets_struct(t: FleetTable, ptr) -> HaldaFleetsC:
     s.n_fleets = t.n_fleets
     sz = t.sizes()
     s.min_devices, s.max_devices = int(sz.min()), int(sz.max())
-    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS:
+    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + BYTE_FIELDS:
         setattr(s, f, ptr(f))
     return s
 
@@ -434,9 +436,9 @@ def _host_struct(t: FleetTable) -> tuple:
     blocks = getattr(t, "_blocks", None)
     if blocks is None:
         arrs = {f: np.ascontiguousarray(getattr(t, f)) for f in ("dev_off", "os_class", "flags") + F64_FIELDS
-                + I64_FIELDS}
+                + BYTE_FIELDS}
         return _fleets_struct(t, lambda f: arrs[f].ctypes.data), arrs
-    off, u8, f64, i64 = blocks
+    off, u8, f64, b64 = blocks
     nd = u8.shape[1]
     s = HaldaFleetsC()
     s.n_fleets = t.n_fleets
@@ -446,11 +448,11 @@ def _host_struct(t: FleetTable) -> tuple:
         sz = np.diff(off)
         s.min_devices, s.max_devices = int(sz.min()), int(sz.max())
     s.dev_off = off.ctypes.data
-    pu, pf, pi = u8.ctypes.data, f64.ctypes.data, i64.ctypes.data
+    pu, pf, pi = u8.ctypes.data, f64.ctypes.data, b64.ctypes.data
     s.os_class, s.flags = pu, pu + nd
     for j, f in enumerate(F64_FIELDS):
         setattr(s, f, pf + 8 * nd * j)
-    for j, f in enumerate(I64_FIELDS):
+    for j, f in enumerate(BYTE_FIELDS):
         setattr(s, f, pi + 8 * nd * j)
     return s, blocks
 
@@ -506,19 +508,19 @@ class _OneFleet:
         self.nd, self.ks, self.L = nd, list(ks), L
         self.karr = np.asarray(self.ks, np.int32)
         self.f64 = np.empty((len(F64_FIELDS), nd))
-        self.i64 = np.empty((len(I64_FIELDS), nd), np.int64)
+        self.b64 = np.empty((len(BYTE_FIELDS), nd))
         self.u8 = np.empty((2, nd), np.uint8)
         self.off = np.empty(2, np.int64)
         self.heads = np.empty(1, np.int64)
         self.consts = np.empty(3)
         # halda_fleets: {int32 n_fleets, min_devices, max_devices; 19 pointers} = 21 u64 slots
         self.hdr = np.zeros(21, np.uint64)
-        pu, pf, pi = self.u8.ctypes.data, self.f64.ctypes.data, self.i64.ctypes.data
+        pu, pf, pi = self.u8.ctypes.data, self.f64.ctypes.data, self.b64.ctypes.data
         self.hdr[0] = 1 | (nd << 32)
         self.hdr[1] = nd
         self.hdr[2:5] = [self.off.ctypes.data, pu, pu + nd]
         self.hdr[5:15] = pf + 8 * nd * np.arange(len(F64_FIELDS), dtype=np.uint64)
-        self.hdr[15:21] = pi + 8 * nd * np.arange(len(I64_FIELDS), dtype=np.uint64)
+        self.hdr[15:21] = pi + 8 * nd * np.arange(len(BYTE_FIELDS), dtype=np.uint64)
         self.fs = HaldaFleetsC.from_buffer(self.hdr)
         xs = 7 * nd + 1
         # x / c only of the k that can be optimal (L // k >= M: every device needs a layer), in the compact
@@ -555,7 +557,7 @@ def pack_one(devs: Sequence[DeviceProfile], model: ModelProfile, ks: Sequence[in
     ws = getattr(_TLS, "one", None)
     if ws is None or ws.nd != nd or ws.ks != ks or ws.L != model.L:
         ws = _TLS.one = _OneFleet(nd, ks, model.L)
-    _PACKER.pack([devs], model.Q, "b_1" in model.f_q, "b_1" in model.f_out, ws.f64, ws.i64, ws.u8, ws.off, ws.heads)
+    _PACKER.pack([devs], model.Q, "b_1" in model.f_q, "b_1" in model.f_out, ws.f64, ws.b64, ws.u8, ws.off, ws.heads)
     return ws
 
 
@@ -575,7 +577,7 @@ def sweep_one(ws: "_OneFleet", model: ModelProfile, kv_factor: float, device: in
         raise RuntimeError(f"halda_solve_fleets_host failed ({rc}): {last_error(lib)}")
     fo = model.f_out
     has_o = "b_1" in fo
-    _PACKER.consts(ws.f64, ws.i64, ws.u8, ws.off, ws.heads, has_o, float(fo["b_1"]) if has_o else 0.0,
+    _PACKER.consts(ws.f64, ws.b64, ws.u8, ws.off, ws.heads, has_o, float(fo["b_1"]) if has_o else 0.0,
                    float(model.b_in), float(model.b_out), float(model.V), ws.consts)
     return ws
 
@@ -668,7 +670,7 @@ class DeviceFleetTable:
         self.table = table
         self.ks = np.asarray([int(k) for k in ks], np.int32)
         self.arrs = {f: torch.from_numpy(np.ascontiguousarray(getattr(table, f))).to(torch_device)
-                     for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS}
+                     for f in ("dev_off", "os_class", "flags") + F64_FIELDS + BYTE_FIELDS}
         nf, nd, nk = table.n_fleets, table.n_devices, len(self.ks)
         self.out = {"best_k": torch.empty(nf, dtype=torch.int32, device=torch_device),
                     "obj_value": torch.empty(nf, dtype=torch.float64, device=torch_device),

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define HALDA_ABI_VERSION 2
+#define HALDA_ABI_VERSION 3
 
 /* per-instance status (halda_result.status) */
 #define HALDA_STATUS_OPTIMAL 0       /* res.success == True                   */
@@ -189,8 +189,9 @@ typedef struct halda_fleets {
     const double *scpu_b1, *sgpu_b1;  /* FLOP/s for batch 1 at quantization Q */
     const double *T_cpu, *T_gpu;      /* T_gpu: the load throughput matching the GPU table */
     const double *t_kvcpy_cpu, *t_kvcpy_gpu, *t_ram2vram, *t_vram2ram, *t_comm, *s_disk;
-    const int64_t *d_avail_ram, *c_cpu, *c_gpu, *d_avail_cuda, *d_avail_metal;
-    const int64_t *swap;              /* min(d_bytes_can_swap, d_swap_avail) for android, else 0 */
+    /* byte counts: the profiles' integers as doubles (exact below 2^53 bytes; ABI 3 -- ABI 2 had int64) */
+    const double *d_avail_ram, *c_cpu, *c_gpu, *d_avail_cuda, *d_avail_metal;
+    const double *swap;               /* min(d_bytes_can_swap, d_swap_avail) for android, else 0 */
 } halda_fleets;
 
 typedef struct halda_fleet_result {

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version_and_lds_budget(lib):
-    assert lib.halda_version() == 2
+    assert lib.halda_version() == 3
     # C3 shape: M = 64 (449 cols), R + 1 = 17 extra-layer states -> well under 160 KiB
     b = lib.halda_lds_bytes(449, 17, 64 * 17, 0)
     assert 0 < b < 64 * 1024

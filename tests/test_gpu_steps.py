@@ -10,7 +10,7 @@ import pytest
 
 from distilp_amd.common import DeviceProfile
 from distilp_amd.solver._libhalda import HaldaContext, get_context
-from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, solve_table
+from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS, fleet_table, solve_table
 from distilp_amd.synth import synth_fleet
 
 pytestmark = pytest.mark.gpu
@@ -25,9 +25,9 @@ def _tiled(model, M, n_base, nf, seed):
                        model)
     reps = -(-nf // n_base)
     big = replace(base, dev_off=np.arange(n_base * reps + 1, dtype=np.int64) * M,
-                  **{f: np.tile(getattr(base, f), reps) for f in ("os_class", "flags") + F64_FIELDS + I64_FIELDS})
+                  **{f: np.tile(getattr(base, f), reps) for f in ("os_class", "flags") + F64_FIELDS + BYTE_FIELDS})
     big = replace(big, dev_off=big.dev_off[:nf + 1],
-                  **{f: getattr(big, f)[:nf * M] for f in ("os_class", "flags") + F64_FIELDS + I64_FIELDS})
+                  **{f: getattr(big, f)[:nf * M] for f in ("os_class", "flags") + F64_FIELDS + BYTE_FIELDS})
     return big.perturbed(np.random.default_rng(seed))
 
 
@@ -99,7 +99,7 @@ def test_group_batches_see_in_place_rewrites(llama_online_model):
     for d in dts:
         _check(d, want, False)
     moved = table.perturbed(np.random.default_rng(9))
-    for f in F64_FIELDS + I64_FIELDS:
+    for f in F64_FIELDS + BYTE_FIELDS:
         dts[1].arrs[f].copy_(torch.from_numpy(np.ascontiguousarray(getattr(moved, f))))
     group.launch(1, 1, stream.cuda_stream)
     torch.cuda.synchronize(dev)

@@ -322,7 +322,7 @@ def test_prepared_plan_equals_solve_fleets(llama_online_model, sizes):
     rewritten in place between launches (a re-profiled fleet stream, config C5) is solved as rewritten."""
     import torch
 
-    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, DeviceFleetTable
+    from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS, DeviceFleetTable
 
     ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
     dev = torch.device("cuda", 0)
@@ -342,7 +342,7 @@ def test_prepared_plan_equals_solve_fleets(llama_online_model, sizes):
         assert np.array_equal(dt.out["obj_by_k"].cpu().numpy(), want.obj_by_k.ravel())
     rng = np.random.default_rng(5)
     moved = table.perturbed(rng)
-    for f in F64_FIELDS + I64_FIELDS:  # rewrite the resident table in place
+    for f in F64_FIELDS + BYTE_FIELDS:  # rewrite the resident table in place
         dt.arrs[f].copy_(torch.from_numpy(np.ascontiguousarray(getattr(moved, f))))
     want2 = solve_table(moved, llama_online_model, ks, 0.5)
     dt.launch(ctx, stream.cuda_stream)

@@ -152,7 +152,7 @@ def test_c_packer_equals_python_packer(llama_online_model):
 
     from distilp_amd.common import DeviceProfile
     from distilp_amd.solver import fleets as fleets_mod
-    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, _host_struct, fleet_table, fleet_table_py
+    from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS, _host_struct, fleet_table, fleet_table_py
     from distilp_amd.synth import synth_fleet
 
     assert fleets_mod._PACKER is not None, "the C packer is not built for this interpreter"
@@ -163,7 +163,7 @@ def test_c_packer_equals_python_packer(llama_online_model):
     t.T_cpu = t.T_cpu * 2
     s, keep = _host_struct(t)
     assert not hasattr(t, "_blocks") and s.T_cpu == keep["T_cpu"].ctypes.data
-    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS:
+    for f in ("dev_off", "os_class", "flags") + F64_FIELDS + BYTE_FIELDS:
         assert getattr(a, f).dtype == getattr(b, f).dtype and np.array_equal(getattr(a, f), getattr(b, f)), f
 
     def err(fn):
@@ -193,14 +193,14 @@ def test_c_packer_equals_python_packer(llama_online_model):
     code = (
         "import sys, numpy as np; sys.path.insert(0, '.');"
         "from tests.conftest import *; from distilp_amd.common import DeviceProfile;"
-        "from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS, fleet_table, fleet_table_py;"
+        "from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS, fleet_table, fleet_table_py;"
         "from distilp_amd.synth import synth_fleet, load_model_dict;"
         "from distilp_amd.common import ModelProfileSplit;"
         "m = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile();"
         "fl = [[DeviceProfile.model_validate(d) for d in synth_fleet(900 + s, 1 + (s * 5) % 64)] for s in range(200)];"
         "fl[7] = [d.model_copy(update={'os_type': 'android', 'd_bytes_can_swap': 7, 'd_swap_avail': 5}) for d in fl[7]];"
         "a, b = fleet_table(fl, m), fleet_table_py(fl, m);"
-        "assert all(np.array_equal(getattr(a, f), getattr(b, f)) for f in ('dev_off', 'os_class', 'flags') + F64_FIELDS + I64_FIELDS);"
+        "assert all(np.array_equal(getattr(a, f), getattr(b, f)) for f in ('dev_off', 'os_class', 'flags') + F64_FIELDS + BYTE_FIELDS);"
         "bad = fl[:50] + [[fl[50][0].model_copy(update={'T_cpu': 0.0})] + fl[50][1:]];"
         "e = None\ntry: fleet_table(bad, m)\nexcept ZeroDivisionError as x: e = x\nassert e is not None;"
         "miss = fl[:9] + [[fl[9][0].model_copy(update={'scpu': {m.Q: {'b_2': 1.0}}})] + fl[9][1:]];"

@@ -34,10 +34,10 @@ def tiled(table, n):
     """n copies of a one-fleet table."""
     from dataclasses import replace
 
-    from distilp_amd.solver.fleets import F64_FIELDS, I64_FIELDS
+    from distilp_amd.solver.fleets import F64_FIELDS, BYTE_FIELDS
 
     M = table.n_devices
-    upd = {f: np.tile(getattr(table, f), n) for f in ("os_class", "flags") + F64_FIELDS + I64_FIELDS}
+    upd = {f: np.tile(getattr(table, f), n) for f in ("os_class", "flags") + F64_FIELDS + BYTE_FIELDS}
     return replace(table, dev_off=np.arange(n + 1, dtype=np.int64) * M, **upd)
 
 
@@ -52,7 +52,7 @@ def main():
 
     from distilp_amd.common import DeviceProfile, ModelProfileSplit
     from distilp_amd.solver._libhalda import get_context
-    from distilp_amd.solver.fleets import (F64_FIELDS, I64_FIELDS, HaldaFleetResultC, _bind, _fleets_struct,
+    from distilp_amd.solver.fleets import (F64_FIELDS, BYTE_FIELDS, HaldaFleetResultC, _bind, _fleets_struct,
                                            fleet_table, model_struct, solve_table)
     from distilp_amd.synth import load_model_dict, synth_fleet
 
@@ -73,7 +73,7 @@ def main():
     for _ in range(2):
         t = big.perturbed(rng)
         arrs = {f: torch.from_numpy(np.ascontiguousarray(getattr(t, f))).to(dev)
-                for f in ("dev_off", "os_class", "flags") + F64_FIELDS + I64_FIELDS}
+                for f in ("dev_off", "os_class", "flags") + F64_FIELDS + BYTE_FIELDS}
         outs = {"best_k": torch.empty(B, dtype=torch.int32, device=dev),
                 "obj_value": torch.empty(B, dtype=torch.float64, device=dev),
                 "w": torch.empty(t.n_devices, dtype=torch.int32, device=dev),
