@@ -35,17 +35,18 @@ def per_kernel(csv_path, counter):
 
 
 def by_grid(trace_csv, out_csv):
-    """Per (kernel, grid size) launch statistics: separates the C3 launches from the bench's small
-    time-to-optimal launches (the --stats summary averages over both)."""
+    """Per (kernel, grid size x, y) launch statistics: separates the C3 launches from the bench's small
+    time-to-optimal launches, and a group launch's K (grid y) from its warm-up's (the --stats summary
+    averages over all of them)."""
     d = defaultdict(list)
     for r in csv.DictReader(open(trace_csv)):
         if "halda" in r["Kernel_Name"]:
-            d[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
+            d[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r.get("Grid_Size_Y") or 1))].append(
                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     with open(out_csv, "w") as f:
-        f.write('"Name","Grid_Size_X","Calls","AverageNs","MinNs","MaxNs"\n')
-        for (k, g), v in sorted(d.items()):
-            f.write(f'"{k}",{g},{len(v)},{statistics.mean(v):.1f},{min(v)},{max(v)}\n')
+        f.write('"Name","Grid_Size_X","Grid_Size_Y","Calls","AverageNs","MinNs","MaxNs"\n')
+        for (k, g, gy), v in sorted(d.items()):
+            f.write(f'"{k}",{g},{gy},{len(v)},{statistics.mean(v):.1f},{min(v)},{max(v)}\n')
 
 
 def main(R):
