@@ -1488,6 +1488,8 @@ int group_check(FleetsGroup *G) {
         int64_t base = 0;  // dev_off[0] of the table (device memory, read once here)
         HIP_TRY(hipMemcpy(&base, P.F.dev_off, sizeof base, hipMemcpyDeviceToHost));
         h[i].base = base;
+        // the steps kernel indexes the table's arrays with 32-bit byte offsets (load_fields32)
+        if (reg && (base < 0 || base + int64_t(P.F.n_fleets) * P0.p.A.uM > (int64_t(1) << 29))) return HALDA_OK;
     }
     if (!G->desc) HIP_TRY(hipMalloc(&G->desc, sizeof(StepsDesc) * h.size()));
     HIP_TRY(hipMemcpy(G->desc, h.data(), sizeof(StepsDesc) * h.size(), hipMemcpyHostToDevice));

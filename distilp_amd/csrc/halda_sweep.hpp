@@ -73,6 +73,26 @@ __device__ inline DevFields load_fields(const halda_fleets &F, int64_t g) {
     return f;
 }
 
+// load_fields with a 32-bit device index (the table's arrays below 4 GiB: the host checks): each load is
+// the array's base in SGPRs plus one shared 32-bit byte offset, no per-field 64-bit address arithmetic
+// (the steps kernel: 864 -> 845 VALU per C3 item).
+template <class T>
+__device__ inline T at32(const T *p, uint32_t boff) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(p) + boff);
+}
+__device__ inline DevFields load_fields32(const halda_fleets &F, uint32_t g) {
+    const uint32_t o8 = g * 8u;
+    DevFields f;
+    f.scpu = at32(F.scpu_b1, o8); f.sgpu = at32(F.sgpu_b1, o8); f.Tc = at32(F.T_cpu, o8); f.Tg = at32(F.T_gpu, o8);
+    f.tkc = at32(F.t_kvcpy_cpu, o8); f.tkg = at32(F.t_kvcpy_gpu, o8); f.r2v = at32(F.t_ram2vram, o8);
+    f.v2r = at32(F.t_vram2ram, o8); f.tcomm = at32(F.t_comm, o8); f.sdisk = at32(F.s_disk, o8);
+    f.ram = at32(F.d_avail_ram, o8); f.ccpu = at32(F.c_cpu, o8); f.cgpu = at32(F.c_gpu, o8);
+    f.cuda = at32(F.d_avail_cuda, o8); f.metal = at32(F.d_avail_metal, o8); f.swap = at32(F.swap, o8);
+    f.cls = at32(F.os_class, g);
+    f.flags = at32(F.flags, g);
+    return f;
+}
+
 // The model as the sweep kernels see it: halda_model plus the uniform quotient (b_in / V) + b_out
 // formed once on the host (the same IEEE double operations, -ffp-contract=off: the same bits) instead
 // of by every wave.
@@ -1148,7 +1168,8 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void h
     cur.kj = A.ks[kl ? lane : 0];
     cur.Wj = kl ? A.Ws[lane] : 0;
     cur.d0 = steps_desc(G, b).base + int64_t(f) * M;
-    cur.mf = load_fields(steps_fleets(steps_desc(G, b)), cur.d0 + (lane < M ? lane : 0));
+    // 32-bit device index: group_check admits tables of at most 2^29 devices here
+    cur.mf = load_fields32(steps_fleets(steps_desc(G, b)), uint32_t(cur.d0 + (lane < M ? lane : 0)));
     sweep_fleet<false, false, Wave, true>(A, steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), f, w, wv,
                                           &cur);
 }
