@@ -1158,7 +1158,8 @@ __global__ __launch_bounds__(64 * kSweepWavesPerBlock, HALDA_STEPS_WAVES) void h
     const int lane = int(threadIdx.x & 63);
     const int nf = A.F.n_fleets, M = A.uM;
     if (f >= nf) return;
-    const int b = int((int64_t(G.first) + blockIdx.y) % G.n_desc);
+    // 32-bit: first < n_desc and blockIdx.y < 65,536 (a 64-bit modulo is ~100 scalar instructions per wave)
+    const int b = int((unsigned(G.first) + blockIdx.y) % unsigned(G.n_desc));
     __shared__ uint8_t dparg[kSweepWavesPerBlock][64 * kDpLanes];
     WaveCtx w = {};
     w.dparg = dparg[threadIdx.x >> 6];
@@ -1886,8 +1887,9 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_steps_kernel
     const int nf = A.F.n_fleets;
     const int ng = int(gridDim.x);
     const int t = int(blockIdx.y), gg = int(blockIdx.x);
-    const int g = int((int64_t(gg) + int64_t(t) * kKslotRot) % ng);
-    const int b = int((int64_t(G.first) + t) % G.n_desc);
+    // 32-bit: gg < ng, t < 65,536, first < n_desc
+    const int g = int((unsigned(gg) + unsigned(t) * unsigned(kKslotRot)) % unsigned(ng));
+    const int b = int((unsigned(G.first) + unsigned(t)) % unsigned(G.n_desc));
     kslot_group(A, SA, SweepBatch{steps_fleets(steps_desc(G, b)), steps_out(steps_desc(G, b)), G.fflag + int64_t(b) * nf},
                 g, smem, kslot_crit(SA));
 }
@@ -1897,7 +1899,7 @@ __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_steps_kernel
 __global__ __launch_bounds__(64, HALDA_SOLVE_WAVES_PER_SIMD) void halda_sweep_tables_steps_kernel(SweepArgs A,
                                                                                                 StepsArgs G) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int b = int((int64_t(G.first) + blockIdx.y) % G.n_desc);
+    const int b = int((unsigned(G.first) + blockIdx.y) % unsigned(G.n_desc));
     const halda_fleets F = steps_fleets(steps_desc(G, b));
     const FleetOut O = steps_out(steps_desc(G, b));
     sweep_body<true, false>(A, SweepBatch{F, O, G.fflag + int64_t(b) * A.F.n_fleets}, smem);
