@@ -1865,14 +1865,16 @@ __device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) 
 // w, pv = rec_pv, own = rec_own), and the tie rule "smaller cost, then smaller n". The record's NaN
 // flag (rec_nanx) is applied by the caller: it fails the whole split, as a NaN cost at every
 // candidate does.
-__device__ inline void rec_try(const FieldRec &r, double aw, double pv, bool own, int w, int nn, int nL, int nU,
+__device__ inline void rec_try(const FieldRec &r, double aw, double pv, double pvo, int w, int nn, int nL, int nU,
                                double &best, int &bn) {
     nn = min(max(nn, nL), nU);
     const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
     double g = aw;
     g = g + r.b * double(nn);
-    const double gs = g + pv * double(sc);
-    g = own ? gs : g;
+    // the class slack's term, priced pvo = (own ? pv : +0): without a class slack it adds +0 * sc = +0, which
+    // leaves g's bits unchanged (g is never -0: aw = alpha w >= +0) -- dev_cost's select, without the
+    // per-try select
+    g = g + pvo * double(sc);
     g = g + pv * double(t);
     const bool better = (g < best) | ((g == best) & (nn < bn));
     best = better ? g : best;
@@ -1896,14 +1898,14 @@ __device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int 
     int nL, nU;
     const bool okI = rec_interval(r, w, nL, nU);
     const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
+    const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
     const bool hc = r.cls == 3 && r.Kset != kNoRow, hv = r.Kvram != kNoRow;
-    if (!kUniform || hc) rec_try(r, aw, pv, own, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
-    if (!kUniform || hv) rec_try(r, aw, pv, own, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
+    if (!kUniform || hc) rec_try(r, aw, pv, pvo, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
+    if (!kUniform || hv) rec_try(r, aw, pv, pvo, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
@@ -1923,11 +1925,11 @@ __device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, 
     int nL, nU;
     const bool okI = rec_interval(r, w, nL, nU);
     const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
+    const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, own, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, nU, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
@@ -1945,12 +1947,12 @@ __device__ inline bool split_second(const FieldRec &r, int w, double &g, int &n,
     int nL, nU;
     const bool okI = rec_interval(r, w, nL, nU);
     const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
+    const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, own, w, 0, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, 1, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, 2, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, 0, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, 1, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, 2, nL, nU, best, bn);
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
@@ -1967,11 +1969,11 @@ __device__ inline bool split_step(const FieldRec &r, int w, int n_prev, double &
     int nL, nU;
     const bool okI = rec_interval(r, w, nL, nU);
     const double pv = rec_pv(r), aw = r.alpha * double(w);
-    const bool own = rec_own(r);
+    const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, own, w, n_prev, nL, nU, best, bn);
-    rec_try(r, aw, pv, own, w, n_prev + 1, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, n_prev, nL, nU, best, bn);
+    rec_try(r, aw, pv, pvo, w, n_prev + 1, nL, nU, best, bn);
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
