@@ -126,3 +126,45 @@ def test_sharded_latency_mode_emulated_ranks(world):
             for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status"):
                 assert torch.equal(a.out[f], b.out[f]), (world, rank, f)
         assert (a.out["best_k"] > 0).all()
+
+
+def test_emulated_sharding_rejects_bad_k_lists_before_any_allocation():
+    """halda_solve_fleets_sharded_emulated checks n_k (1..1024) and the k list (ascending, unique, > 0)
+    before it sizes or reallocates its per-rank scratch: each bad call is HALDA_E_ARG (-22), not a HIP
+    error from a wrapped size, and a good call afterwards still returns the single-GPU sweep's results."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from distilp_amd.common import DeviceProfile, ModelProfileSplit
+    from distilp_amd.solver._libhalda import get_context
+    from distilp_amd.solver.fleets import DeviceFleetTable, _bind, fleet_table, launch_sharded_emulated
+    from distilp_amd.synth import load_model_dict, synth_fleet
+
+    m2 = ModelProfileSplit.model_validate(load_model_dict()).to_model_profile()
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    stream = torch.cuda.Stream(dev)
+    table = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(3400 + s, 16)] for s in range(20)], m2)
+    a = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+    a.launch(ctx, stream.cuda_stream)
+    b = DeviceFleetTable(table, m2, ks, 0.5, dev, want_per_k=True)
+    launch_sharded_emulated(b, ctx, 2, 0, stream.cuda_stream)  # the scratch exists before the bad calls
+    lib = _bind(ctx.lib)
+    bad = [(-1, ks), (0, ks), (2000, ks), (3, [2, 1, 4]), (2, [1, 1]), (2, [0, 1]), (2, [-2, 1])]
+    for n_k, kl in bad:
+        karr = np.zeros(max(len(kl), 1), np.int32)
+        karr[:len(kl)] = kl
+        with ctx._lock:
+            rc = lib.halda_solve_fleets_sharded_emulated(ctx.ctx, 2, 0, ctypes.byref(b.model), ctypes.byref(b.fs),
+                                                         karr.ctypes.data, n_k, ctypes.byref(b.res),
+                                                         ctypes.c_void_p(stream.cuda_stream))
+        assert rc == -22, (n_k, kl, rc)
+    for t in b.out.values():
+        t.fill_(-7)
+    launch_sharded_emulated(b, ctx, 2, 1, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status"):
+        assert torch.equal(a.out[f], b.out[f]), f

@@ -207,3 +207,33 @@ def test_kslot_group_launch_with_hand_backs(llama_online_model, first, steps):
     for d, w in zip(tabs, wants):
         _check(d, w, True)
     group.close()
+
+
+def test_rotation_over_kslot_tables_of_different_lds(llama_online_model):
+    """Prepared k-slot launches whose dynamic LDS differs (C2's 16-device fleets at L = 80, about 40 KiB,
+    and at L = 160, above 64 KiB for the k = 2 slot's tables) in one rotation: the kernel's LDS attribute
+    only ever grows (Ctx::ensure_lds), so the larger plan's launches are not refused or mis-sized after
+    the smaller one ran, and every table's results equal its own solve."""
+    import torch
+
+    from distilp_amd.solver.fleets import DeviceFleetTable, PlanRotation
+
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    models = [llama_online_model, llama_online_model.model_copy(update={"L": 160})]
+    tabs, wants = [], []
+    for i, model in enumerate(models):
+        ks = [d for d in range(1, model.L) if model.L % d == 0 and d <= 40]
+        table = _tiled(model, 16, 8, 200, 36000 + 7 * i)
+        wants.append(solve_table(table, model, ks, 0.5))
+        tabs.append(DeviceFleetTable(table, model, ks, 0.5, dev, want_per_k=True))
+    stream = torch.cuda.Stream(dev)
+    rot = PlanRotation(tabs, ctx, [stream.cuda_stream])
+    for t in tabs:
+        for v in t.out.values():
+            v.zero_()
+    torch.cuda.synchronize(dev)
+    rot.launch(0, 5)
+    torch.cuda.synchronize(dev)
+    for d, w in zip(tabs, wants):
+        _check(d, w, True)
