@@ -866,6 +866,20 @@ def main():
     sweep_group(max(args.warmup, 1))
     torch.cuda.synchronize(dev)
     el_sweep = timed(None, args.steps, torch, dev, dist, world, tag="headline", many=sweep_group)
+    if os.environ.get("HALDA_BENCH_REPEAT"):  # diagnostic: the same region again, timings on stderr
+        again, evs = [], []
+        for _ in range(int(os.environ["HALDA_BENCH_REPEAT"])):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            sweep_group(args.steps)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            again.append(time.perf_counter() - t0)
+            evs.append(e0.elapsed_time(e1) * 1e-3)
+        print(f"bench: headline region {el_sweep * 1e6:.1f} us, repeated (wall, events): "
+              f"{[(round(a * 1e6, 1), round(b * 1e6, 1)) for a, b in zip(again, evs)]}", file=sys.stderr)
     el_sweep2 = timed(sweep_step, args.steps, torch, dev, dist, world, tag="per_launch", many=sweep_many)
     el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world, many=sweep_many_one_stream)
     sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream, many=sweep_many_one_stream)
