@@ -1865,9 +1865,12 @@ __device__ inline bool rec_interval(const FieldRec &r, int w, int &nL, int &nU) 
 // w, pv = rec_pv, own = rec_own), and the tie rule "smaller cost, then smaller n". The record's NaN
 // flag (rec_nanx) is applied by the caller: it fails the whole split, as a NaN cost at every
 // candidate does.
+// kClamp = false: nn is nL or nU itself, which needs no clamp (when nL > nU the split fails whatever the
+// tries give)
+template <bool kClamp = true>
 __device__ inline void rec_try(const FieldRec &r, double aw, double pv, double pvo, int w, int nn, int nL, int nU,
                                double &best, int &bn) {
-    nn = min(max(nn, nL), nU);
+    if constexpr (kClamp) nn = min(max(nn, nL), nU);
     const int sc = max(0, w - (r.cls == 3 ? nn : 0) + r.Kset), t = max(0, nn + r.Kvram);  // kNoRow: 0
     double g = aw;
     g = g + r.b * double(nn);
@@ -1901,8 +1904,8 @@ __device__ inline bool split_full_impl(const FieldRec &r, int w, double &g, int 
     const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
+    rec_try<false>(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
+    rec_try<false>(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
     const bool hc = r.cls == 3 && r.Kset != kNoRow, hv = r.Kvram != kNoRow;
     if (!kUniform || hc) rec_try(r, aw, pv, pvo, w, hc ? w + r.Kset : nL, nL, nU, best, bn);  // class-slack kink
     if (!kUniform || hv) rec_try(r, aw, pv, pvo, w, hv ? -r.Kvram : nL, nL, nU, best, bn);     // VRAM kink
@@ -1928,8 +1931,8 @@ __device__ inline bool split_first(const FieldRec &r, int w, double &g, int &n, 
     const double pvo = rec_own(r) ? pv : 0.0;
     double best = kInf;
     int bn = -1;
-    rec_try(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
-    rec_try(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
+    rec_try<false>(r, aw, pv, pvo, w, nL, nL, nU, best, bn);
+    rec_try<false>(r, aw, pv, pvo, w, nU, nL, nU, best, bn);
     const bool ok = okI & (bn >= 0) & !rec_nanx(r);
     if (ok) {
         g = best;
