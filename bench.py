@@ -1,33 +1,25 @@
 """Benchmark: HALDA MILP instances solved/s on MI355X (config C3 of BASELINE.json).
 
-Headline workload per GPU and step (weak scaling, the default): 4096 seeded synthetic
-fleets of M = 64 devices (L = 80, model llama_3_70b/online, kv "4bit"), each swept over
-all 9 k-candidates of L = 80 -> 36,864 fixed-k MILP instances, i.e. 4096 `halda_solve`
-k-sweeps: ONE libhalda `halda_solve_fleets` call per step takes the fleets' device-field
-table (resident in HBM) through the whole reference path -- lowering of every (fleet, k)
-(halda_p_solver.py:59-338), the exact solves (:340-353) and the argmin over k with the
-reference's tie rule (:391-414). Nothing is pre-lowered on the host. Consecutive steps are
-independent batches (own resident tables and results) and alternate between two HIP streams, as
-a streaming deployment keeps two batches in flight: one batch's field loads overlap the previous
-batch's compute. `one_stream` gives the same steps serialised on one stream; the roofline's
-kernel time is the one-stream launch time (HIP events around K launches), `roofline.pipelined`
-the same bytes over the two-stream step time.
+Headline workload per GPU and step (weak scaling, the default): 4096 seeded synthetic fleets of M = 64
+devices (L = 80, model llama_3_70b/online, kv "4bit"), each swept over all 9 k-candidates of L = 80 ->
+36,864 fixed-k MILP instances, i.e. 4096 `halda_solve` k-sweeps. Every step takes the fleets' device-field
+table (resident in HBM, 16 rotating copies > the Infinity Cache) through the whole reference path -- the
+lowering of every (fleet, k) (halda_p_solver.py:59-338), the exact solves (:340-353) and the argmin over k
+with the reference's tie rule (:391-414). The K timed steps are ONE group launch (halda_fleets_group_launch
+-> halda_sweep_steps_kernel), bit-identical per batch to K launches (checked before timing).
 
-Beside it, in the same JSON line:
-  solve_only   the pre-lowered batch (host lowering, CSR in HBM) through the milp()
-               replacement alone (halda_solve_batch_device), with its own roofline;
-  strong       (N > 1) config C3 as a strong-scaling sweep: 4096 fleets in total, sharded
-               over the ranks (shard_bounds), max time over ranks;
-  cpu_baseline the oracle (reference lowering + scipy 1.15 / HiGHS 1.8.0, the reference's
-               arithmetic) on every host core this process may use, one pinned process per
-               core, on a bounded sample of the same fleets; also the 1-core rate;
-  time_to_optimal_ms  median wall time of one M = 64 halda_solve (Python call -> HALDAResult),
-               100 runs.
-Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, before any
-GPU call in this process) unless it already runs as one of them (WORLD_SIZE set, e.g. by the
-driver's own torch.distributed.run); --gpus must equal the world size it sees and the node
-must have N GPUs, else it exits with an error. Fleets are independent: no collective on the
-data path, a barrier brackets each timed region and the max time over ranks is reported.
+The ONE JSON line (compact_line: <= 3.5 KB) carries beside the headline: the roofline of the headline's
+launch (HBM and VALU issue), the CPU baseline (the oracle -- reference lowering + scipy / HiGHS 1.8.0 -- on
+the host cores, pinned), the per-batch launches, latency mode, the C5 stream, the public batch API, the
+milp() replacement on a pre-lowered CSR batch (solve_only), config C2 (4096 M = 16 fleets, k > 1 MILPs),
+feasible-only instances/s and the time to optimal of one M = 64 halda_solve; DESIGN.md §5 defines each.
+`--full-json PATH` writes the detailed record.
+
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, before any GPU call in
+this process) unless it already runs as one of them (WORLD_SIZE set, e.g. by the driver's own
+torch.distributed.run); --gpus must equal the world size it sees and the node must have N GPUs, else it
+exits with an error. Fleets are independent: no collective on the data path. Each rank times its own
+region between a barrier and its device's synchronize; the max over ranks is reported (timed()).
 """
 
 from __future__ import annotations
@@ -48,12 +40,13 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-# FP64-VALU-issue roof beside the HBM one: a wave64 VALU instruction holds its SIMD for >= 4
-# cycles (FP64 add / mul / FMA issue at full rate), 1,024 SIMDs at <= 2.4 GHz. The VALU count per wave is
-# NOT a constant here: it is read from the newest profiles/*_valu.json whose libhalda.so hash equals the
-# library this process loads (tools/valu_stamp.py writes it from a rocprofv3 SQ_INSTS_VALU / SQ_WAVES pass);
-# with no matching profile the VALU roof is reported as null.
-VALU_CYCLES = 4
+# VALU-issue roof beside the HBM one: SIMD cycles per wave64 VALU instruction by type -- FP64
+# add / mul / FMA 4 (16 FP64 lanes per cycle), FP64 transcendentals 8, every other VALU 2 (SIMD-32,
+# MI355X_MICROARCH.md:54) -- on 1,024 SIMDs at <= 2.4 GHz. The counts per item are NOT constants here: they are
+# read from the newest profiles/*_valu.json whose libhalda.so hash equals the library this process loads
+# (tools/valu_stamp.py writes them from rocprofv3 SQ_INSTS_VALU and per-type SQ_INSTS_VALU_* passes); with no
+# matching profile the VALU roof is reported as null.
+VALU_CYCLES = {"fp64": 4, "trans_f64": 8, "other": 2}
 N_SIMDS = 1024
 CLOCK_GHZ = 2.4
 KS_L80 = [1, 2, 4, 5, 8, 10, 16, 20, 40]
@@ -223,10 +216,8 @@ def run_cpu_baseline(budget_s: float, M: int):
         "value": inst / secs, "unit": "instances/s", "cores": len(cores), "kind": "port",
         "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
         "one_core_value": one["instances"] / one["seconds"],
-        "sample": (f"{len(cores)} pinned processes (one per usable core), each the oracle on its own C3 fleets "
-                   f"for ~{budget_s:.0f} s: {sum(r['fleets'] for r in allc)} fleets x 9 k = {inst} instances in "
-                   f"{secs:.1f} s; one core alone: {one['instances']} instances in {one['seconds']:.1f} s. "
-                   "oracle/milp_oracle.py = the reference's lowering + scipy 1.15 HiGHS 1.8.0 (its arithmetic)"),
+        "sample": (f"{len(cores)} pinned procs x ~{budget_s:.0f} s, own C3 fleets: {sum(r['fleets'] for r in allc)} "
+                   f"fleets x 9 k in {secs:.1f} s; oracle/milp_oracle.py (reference lowering + HiGHS 1.8.0)"),
     }
 
 
@@ -234,29 +225,64 @@ def run_cpu_baseline(budget_s: float, M: int):
 HOST_ENQUEUE = {}  # per timed leg: host seconds to enqueue its K steps (before the final synchronize)
 
 
-def timed(step, steps, torch, dev, dist, world, tag=None, many=None):
-    """Seconds for `steps` steps between barrier + synchronize on both sides (max over ranks). `many`,
-    when given, enqueues all of them in one call (the k-sweep legs: halda_fleets_plan_launch_many, one
-    kernel launch per step from C, no Python round trip per step); else step() runs `steps` times."""
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+class Ranks:
+    """The ranks of one bench job: `sync` waits for this rank's device, `barrier` / `max` / `min` are the
+    collectives (no-ops at world 1). The reductions run on the device for RCCL, on the host for gloo."""
+
+    def __init__(self, dist, world: int, sync, device=None):
+        self.dist, self.world, self.sync, self.device = dist, world, sync, device
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def _reduce(self, x: float, op) -> float:
+        if self.world == 1:
+            return x
+        import torch
+
+        on = self.device if self.dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=on)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX if self.world > 1 else None)
+
+    def min(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MIN if self.world > 1 else None)
+
+
+def timed(step, steps, R: Ranks, tag=None, many=None, on_stream=None):
+    """Seconds for `steps` steps, max over ranks. Every rank leaves a barrier, waits for its device, reads
+    the clock, enqueues the steps, waits for its device and reads the clock again: its own elapsed time,
+    taken BEFORE any collective, so neither the closing collective nor a late rank's barrier exit is
+    inside the region; then the all-reduce MAX. `many`, when given, enqueues all steps in one call (one
+    ctypes call); else step() runs `steps` times. `on_stream` = (torch, stream): HIP events recorded on
+    that stream around the steps as well; returns (seconds, event ms of this rank) then."""
+    R.barrier()
+    R.sync()
+    ev = None
+    if on_stream is not None:
+        torch_, stream = on_stream
+        ev = (torch_.cuda.Event(enable_timing=True), torch_.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record(stream)
     if many is not None:
         many(steps)
     else:
         for _ in range(steps):
             step()
+    if ev:
+        ev[1].record(stream)
     if tag:
         HOST_ENQUEUE[tag] = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    R.sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = R.max(elapsed)
+    if ev:
+        return elapsed, ev[0].elapsed_time(ev[1])
     return elapsed
 
 
@@ -301,6 +327,34 @@ def valu_profile(kernel: str, workload: str):
     return None
 
 
+def valu_issue(vp, units: int, ms: float):
+    """VALU-issue roof of a launch of `units` items (or waves, for a per-batch kernel profile) that took
+    `ms`: the SIMD cycles its VALU instructions need at the peak clock over the SIMD cycles available.
+    Priced by type from the build's per-type counters: FP64 add / mul / FMA at 4 cycles per wave64
+    instruction (16 FP64 lanes per cycle per SIMD: 78.6 TF), FP64 transcendentals at 8, every other
+    VALU at 2 (SIMD-32, MI355X_MICROARCH.md:54); `frac_all_at_4` prices every VALU at 4 (one wave alone
+    per SIMD, or every uncounted op on the FP64 pipe), the bound this roof was quoted at before round 6."""
+    if not vp:
+        return {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
+    per = vp["valu_per_wave"] * vp["waves"] / vp.get("items", vp["waves"])  # VALU per unit
+    simd_cycles = N_SIMDS * CLOCK_GHZ * 1e9 * ms * 1e-3
+    out = {"valu_per_item": per, "frac_all_at_4": per * units * 4 / simd_cycles,
+           "wait_any_frac": vp.get("wait_any_frac"), "source": vp["source"]}
+    t = vp.get("valu_types")
+    if t:
+        scale = vp["waves"] / vp.get("items", vp["waves"])
+        fp64 = (t["add_f64"] + t["mul_f64"] + t["fma_f64"]) * scale
+        trans = t["trans_f64"] * scale
+        other = per - fp64 - trans
+        out.update(fp64_per_item=fp64, fp64_trans_per_item=trans, other_per_item=other,
+                   frac=(VALU_CYCLES["fp64"] * fp64 + VALU_CYCLES["trans_f64"] * trans + VALU_CYCLES["other"] * other)
+                   * units / simd_cycles)
+    else:
+        out["frac"] = None
+        out["why"] = "no per-type VALU pass for this build (profiles/run_round.sh)"
+    return out
+
+
 def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None, workload="c3"):
     """Roofline of the dominant launch. phase_ms: per-launch device times (HIP events around each
     launch, one launch at a time). one_launch_ms: when every step is that one launch, its mean time
@@ -316,15 +370,7 @@ def roofline(phase_ms, alg_bytes, traffic_fn, one_launch_ms=None, workload="c3")
     achieved = alg / (ms * 1e-3) / 1e9 if alg else None
     frac = achieved / HBM_PEAK_GBS if achieved else None
     vp = valu_profile(dom, workload)
-    if vp:
-        need = vp["valu_per_wave"] * vp["waves"] * VALU_CYCLES / (N_SIMDS * CLOCK_GHZ * 1e9)
-        valu = {"frac": need / (ms * 1e-3), "valu_per_wave": vp["valu_per_wave"], "waves": vp["waves"],
-                "cycles_per_valu": VALU_CYCLES, "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": vp["source"],
-                "wait_any_frac": vp.get("wait_any_frac"),
-                "what": "FP64-VALU-issue roof of the same launch: VALU cycles its waves need / SIMD cycles in the "
-                        "kernel time (rocprofv3 SQ_INSTS_VALU / SQ_WAVES of this build, peak clock)"}
-    else:
-        valu = {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
+    valu = valu_issue(vp, vp["waves"] if vp else 0, ms)
     roofs = {"hbm": frac, "valu_issue": valu["frac"]}
     nearest = max((k for k, v in roofs.items() if v is not None), key=lambda k: roofs[k], default=None)
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": frac,
@@ -344,15 +390,7 @@ def group_roofline(launch_ms, steps, batch_bytes, n_fleets, single, kern="halda_
     alg = steps * batch_bytes
     achieved = alg / (launch_ms * 1e-3) / 1e9
     vp = valu_profile(kern, workload)
-    if vp and vp.get("items"):
-        # VALU per (fleet, batch) item of the profiled launch, times this launch's items
-        need = vp["valu_per_wave"] * vp["waves"] / vp["items"] * (steps * n_fleets) * VALU_CYCLES / (
-            N_SIMDS * CLOCK_GHZ * 1e9)
-        valu = {"frac": need / (launch_ms * 1e-3), "valu_per_item": vp["valu_per_wave"] * vp["waves"] / vp["items"],
-                "cycles_per_valu": VALU_CYCLES, "simds": N_SIMDS, "clock_ghz": CLOCK_GHZ, "source": vp["source"],
-                "wait_any_frac": vp.get("wait_any_frac")}
-    else:
-        valu = {"frac": None, "why": "no profiles/*_valu.json recorded for this libhalda.so build"}
+    valu = valu_issue(vp if vp and vp.get("items") else None, steps * n_fleets, launch_ms)
     per_batch = pmc_entry(kern, "hbm_bytes_per_batch")
     traffic = per_batch * steps if per_batch is not None else None  # HBM bytes scale with the batches
     roofs = {"hbm": achieved / HBM_PEAK_GBS, "valu_issue": valu["frac"]}
@@ -489,9 +527,7 @@ def batch_api(model, fleets, runs: int = 3):
         one = halda_solve(fleets[0], model, mip_gap=1e-4, plot=False, kv_bits="4bit")
     if (out[0].k, out[0].w, out[0].n, out[0].obj_value) != (one.k, one.w, one.n, one.obj_value):
         raise RuntimeError("halda_solve_batch disagrees with halda_solve")
-    return {"what": f"halda_solve_batch on {len(fleets)} C3 fleets (DeviceProfile lists -> HALDAResult, host-formed "
-                    "objectives), median of the warm calls", "ms": statistics.median(times[1:]),
-            "fleets_per_s": len(fleets) / (statistics.median(times[1:]) * 1e-3)}
+    return {"ms": statistics.median(times[1:]), "fleets_per_s": len(fleets) / (statistics.median(times[1:]) * 1e-3)}
 
 
 def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
@@ -513,10 +549,7 @@ def c5_stream(model, M: int, batches: int = 8, B: int = C3_FLEETS):
         if not (res.best_k > 0).all():
             raise RuntimeError("C5: a re-profiled fleet without a feasible k")
     dt = (time.perf_counter() - t0) / batches
-    return {"what": f"C5: re-profiled M={M} fleet, batches of {B} perturbed instances (host perturbation, PCIe in, "
-                    "k-sweep, PCIe out; synchronous, one batch at a time)",
-            "ms_per_batch": dt * 1e3, "fleets_per_s": B / dt, "instances_per_s": B * len(KS_L80) / dt,
-            "target_instances_per_s": 10_000}
+    return {"ms_per_batch": dt * 1e3, "fleets_per_s": B / dt, "instances_per_s": B * len(KS_L80) / dt}
 
 
 def c2_leg(args, torch, dev, ctx, model, stream, srefs):
@@ -581,9 +614,10 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
 
     manyg(steps)  # warm
     torch.cuda.synchronize(dev)
-    elg = timed(None, steps, torch, dev, None, 1, many=manyg)
+    R1 = Ranks(None, 1, lambda: torch.cuda.synchronize(dev))
+    elg = timed(None, steps, R1, many=manyg)
     evg = statistics.median(timed_events(None, 1, torch, dev, stream, many=lambda _: manyg(steps)) for _ in range(3))
-    el2 = timed(step2, steps, torch, dev, None, 1, many=many2)
+    el2 = timed(step2, steps, R1, many=many2)
     ev1 = timed_events(step1, steps, torch, dev, stream, many=many1)
     ctx.set_timing(True)
     per = []
@@ -595,16 +629,10 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     ph = {k: statistics.mean(p.get(k, 0.0) for p in per) for k in per[0]}
     inst = C3_FLEETS * len(KS_L80)
     return {
-        "workload": f"C2: {C3_FLEETS} synthetic M={M2} fleets x {len(KS_L80)} k-candidates (L=80, llama_3_70b/online, "
-                    "kv 4bit) per step, one halda_solve_fleets k-sweep from resident tables",
         "instances_per_step": inst, "feasible_per_step": n_opt,
         "ms_per_step": elg / steps * 1e3, "instances_per_s": inst * steps / elg,
-        "group_launch": {"persistent": group.persistent, "launch_ms": evg, "ms_per_batch_events": evg / steps,
-                         "alg_GBps": alg * steps / (evg * 1e-3) / 1e9,
-                         "what": "the K steps as one group launch (k-slot steps kernel + the gated table launch), "
-                                 "HIP events around it on its stream, median of 3"},
-        "ms_per_step_one_stream": ev1, "instances_per_s_one_stream": inst / (ev1 * 1e-3),
-        "ms_per_step_two_streams": el2 / steps * 1e3, "instances_per_s_two_streams": inst * steps / el2,
+        "ms_per_batch_events": evg / steps, "group_persistent": group.persistent,
+        "ms_per_step_one_stream": ev1, "ms_per_step_two_streams": el2 / steps * 1e3,
         "steps": steps, "resident_copies": n,
         "roofline": group_roofline(evg, steps, alg, C3_FLEETS,
                                    roofline(ph, {k: alg for k in ph}, pmc_traffic,
@@ -625,7 +653,7 @@ def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
     from distilp_amd.solver.fleets import (DeviceFleetTable, RcclComm, fleet_table, launch_sharded,
                                            launch_sharded_emulated)
 
-    out = {"what": latency_leg.__doc__.split("\n\n")[0].replace("\n    ", " ").strip()}
+    out = {}
     try:
         comm = RcclComm(1, 0, RcclComm.unique_id(), dev.index or 0)
     except Exception as e:  # noqa: BLE001
@@ -671,6 +699,72 @@ def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
     return out
 
 
+def _g(x, n: int = 5):
+    """x rounded to n significant digits (the compact line), None and non-floats unchanged."""
+    return float(f"{x:.{n}g}") if isinstance(x, float) else x
+
+
+def _pick(d, *keys, n: int = 5):
+    return None if d is None else {k: _g(d.get(k), n) for k in keys if d.get(k) is not None}
+
+
+def compact_line(full: dict) -> dict:
+    """The ONE JSON line the bench prints (<= 3.5 KB, so a driver that keeps the last ~4 KB of stdout keeps
+    all of it): the contract's keys first, then each leg's figures, the figures BASELINE's metric names
+    last -- the C5 stream, the batch API, the milp() replacement, C2, feasible-only instances/s and the
+    time to optimal. Every field is defined in DESIGN.md §5; `--full-json` writes the detailed record."""
+    rf = full["roofline"]
+    vi = rf.get("valu_issue") or {}
+    sb = rf.get("single_batch_kernel") or {}
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup")}
+    line["ms_per_step"] = _g(full["ms_per_step"], 6)
+    line.update({k: full[k] for k in ("higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")})
+    line["roofline"] = dict(
+        {k: _g(rf.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms",
+                                     "steps_per_launch")},
+        alg_bytes_per_launch=rf.get("algorithmic_bytes_per_launch"),
+        valu_issue=_pick(vi, "frac", "frac_all_at_4", "valu_per_item", "fp64_per_item", "fp64_trans_per_item",
+                         "other_per_item", "wait_any_frac", n=3),
+        single_batch={"kernel": sb.get("kernel"), "kernel_ms": _g(sb.get("kernel_ms")), "frac": _g(sb.get("frac"), 3)})
+    cb = full.get("cpu_baseline")
+    line["cpu_baseline"] = None if cb is None else dict(
+        _pick(cb, "value", "unit", "cores", "kind", "one_core_value", "nproc"), sample=cb.get("sample"))
+    line["rank_launch_ms"] = _pick(full.get("rank_launch_ms"), "max", "min")
+    line["weak_200"] = _pick(full.get("weak_200"), "ms_per_step", "instances_per_s")
+    line["strong"] = _pick(full.get("strong"), "fleets_total", "ms_per_step", "instances_per_s")
+    line["per_launch_ms_per_step"] = _g(full["per_launch"]["ms_per_step"])
+    line["one_stream_ms_per_step"] = _g(full["one_stream"]["ms_per_step"])
+    line["host_enqueue_ms_per_step"] = _g(full["host_enqueue_ms_per_step"], 3)
+    lat = full.get("latency_mode")
+    if lat:
+        line["latency_mode_device_ms"] = {
+            name: dict({way: _g(lat[name][way]["device_ms_per_call"], 4) for way in ("plain", "rccl_world1")
+                        if way in lat[name]},
+                       world8_rank_max=_g(lat[name]["rank_subsweep_world8"]["max_device_ms"], 4))
+            for name in ("one_fleet", "fleets_4096") if name in lat}
+    line["fleets_per_s"] = _g(full["fleets_per_s"])
+    line["c5_stream"] = _pick(full.get("c5_stream"), "instances_per_s", "ms_per_batch")
+    line["batch_api"] = _pick(full.get("batch_api"), "fleets_per_s", "ms")
+    so = full["solve_only"]
+    line["solve_only"] = dict(
+        _pick(so, "ms_per_step_one_stream", "ms_per_step_no_settled"),
+        roofline=_pick(so["roofline"], "kernel", "kernel_ms", "traffic", "frac"), ms_per_step=_g(so["ms_per_step"]))
+    c2 = full.get("c2")
+    line["c2"] = None
+    if c2:
+        r2 = c2["roofline"]
+        line["c2"] = dict(_pick(c2, "ms_per_batch_events", "ms_per_step_two_streams", "instances_per_s"),
+                          roofline=dict(_pick(r2, "kernel_ms", "traffic"),
+                                        valu_issue_frac=_g((r2.get("valu_issue") or {}).get("frac"), 3),
+                                        frac=_g(r2.get("frac"))),
+                          ms_per_step=_g(c2["ms_per_step"]))
+    line["feasible_instances_per_s"] = _g(full["feasible_instances_per_s"])
+    line["time_to_optimal_parts"] = _pick(full.get("time_to_optimal_parts"), "pack_ms", "gpu_call_ms", "rest_ms",
+                                          "gpu_call_copy_path_ms", n=3)
+    line["time_to_optimal_ms"] = _g(full.get("time_to_optimal_ms"))
+    return line
+
+
 def launch_ranks(args) -> int:
     """--gpus N from a plain `python bench.py`: start N ranks (one process per GPU) with
     torch.distributed.run before this process touches the GPU, relay their output and exit code."""
@@ -705,6 +799,8 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 leg (4096 M = 16 fleets)")
     ap.add_argument("--no-latency", action="store_true", help="skip the latency-mode leg")
     ap.add_argument("--ks", type=str, default="", help="diagnostic: comma-separated k-candidates instead of C3's")
+    ap.add_argument("--full-json", type=str, default="",
+                    help="also write the detailed record (every leg's figures, per-launch times) to this file")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-core", type=int, default=0)
     ap.add_argument("--cpu-first", type=int, default=0)
@@ -865,7 +961,14 @@ def main():
     # checks above left the GPU idle for milliseconds of host work)
     sweep_group(max(args.warmup, 1))
     torch.cuda.synchronize(dev)
-    el_sweep = timed(None, args.steps, torch, dev, dist, world, tag="headline", many=sweep_group)
+    R = Ranks(dist, world, lambda: torch.cuda.synchronize(dev), dev)
+    el_sweep, ev_head = timed(None, args.steps, R, tag="headline", many=sweep_group, on_stream=(torch, stream))
+    # each rank's device time of its group launch (HIP events on its stream inside the region)
+    rank_launch_ms = {"max": R.max(ev_head), "min": R.min(ev_head)}
+    el_200 = None
+    if world > 1:  # beside the driver's K: a 200-step weak-scaling region (one launch of 200 batches)
+        sweep_group(max(args.warmup, 1))
+        el_200 = timed(None, 200, R, many=sweep_group)
     if os.environ.get("HALDA_BENCH_REPEAT"):  # diagnostic: the same region again, timings on stderr
         again, evs = [], []
         for _ in range(int(os.environ["HALDA_BENCH_REPEAT"])):
@@ -880,17 +983,17 @@ def main():
             evs.append(e0.elapsed_time(e1) * 1e-3)
         print(f"bench: headline region {el_sweep * 1e6:.1f} us, repeated (wall, events): "
               f"{[(round(a * 1e6, 1), round(b * 1e6, 1)) for a, b in zip(again, evs)]}", file=sys.stderr)
-    el_sweep2 = timed(sweep_step, args.steps, torch, dev, dist, world, tag="per_launch", many=sweep_many)
-    el_sweep1 = timed(sweep_step_one_stream, args.steps, torch, dev, dist, world, many=sweep_many_one_stream)
+    el_sweep2 = timed(sweep_step, args.steps, R, tag="per_launch", many=sweep_many)
+    el_sweep1 = timed(sweep_step_one_stream, args.steps, R, many=sweep_many_one_stream)
     sweep_ev_ms = timed_events(sweep_step_one_stream, args.steps, torch, dev, stream, many=sweep_many_one_stream)
     # the group launch's own device time (HIP events on its stream around the one launch of K batches)
     group_ms = statistics.median(timed_events(None, 1, torch, dev, stream, many=lambda _: sweep_group(args.steps))
                                  for _ in range(3))
-    el_solve = timed(solve_step, args.steps, torch, dev, dist, world)
-    el_solve1 = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
+    el_solve = timed(solve_step, args.steps, R)
+    el_solve1 = timed(solve_step_one_stream, args.steps, R)
     hint[0] = None  # the same legs without the settled flags: the screen proves every verdict itself
-    el_solve_ns = timed(solve_step, args.steps, torch, dev, dist, world)
-    el_solve1_ns = timed(solve_step_one_stream, args.steps, torch, dev, dist, world)
+    el_solve_ns = timed(solve_step, args.steps, R)
+    el_solve1_ns = timed(solve_step_one_stream, args.steps, R)
     hint[0] = settled_dev.data_ptr()
     el_strong = None
     if world > 1 and not strong_head:
@@ -914,7 +1017,7 @@ def main():
 
         for _ in range(max(args.warmup, len(srefs))):
             strong_step()
-        el_strong = timed(strong_step, args.steps, torch, dev, dist, world, many=strong_many)
+        el_strong = timed(strong_step, args.steps, R, many=strong_many)
 
     # per-launch device times (HIP events recorded by libhalda on the kernels' stream), after the
     # timed regions; the dominant launch of each leg is the longest
@@ -944,7 +1047,7 @@ def main():
         tto, tto_parts = time_to_optimal(model, args.M) if (world == 1 and not args.no_tto) else (None, None)
         c5 = c5_stream(model, args.M) if (world == 1 and not args.no_tto) else None
         bapi = batch_api(model, fleets) if (world == 1 and not args.no_tto) else None
-        line = {
+        full = {
             "metric": METRIC,
             "value": value,
             "unit": "instances/s",
@@ -958,44 +1061,36 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded C3 fleets, distilp_amd/synth.py)",
             "config": {
-                "workload": (f"C3: {len(fleets) if not strong_head else C3_FLEETS} synthetic M={args.M} fleets x "
-                             f"{len(ks)} k-candidates per {'GPU' if not strong_head else 'node'} (L=80, "
-                             "llama_3_70b/online, kv 4bit): one halda_solve_fleets k-sweep per step from the "
-                             "fleets' device-field tables resident in HBM (GPU lowering + exact solves + argmin "
-                             "over k)"),
+                "workload": (f"C3: {len(fleets) if not strong_head else C3_FLEETS} M={args.M} fleets x {len(ks)} k "
+                             f"per {'GPU' if not strong_head else 'node'} (L=80, llama_3_70b/online, kv 4bit), one "
+                             "k-sweep per step from HBM-resident tables"),
                 "instances_per_step_per_gpu": inst_rank,
                 "feasible_per_step_per_gpu": n_opt,
-                "parallelism": f"dp{world} (fleets sharded, no collective on the data path)",
+                "parallelism": f"dp{world}",
                 "rccl_world_size": rccl_world,
                 "resident_copies": n_sw,
             },
-            "launch": {"what": "the K steps as ONE group launch (halda_fleets_group_launch -> "
-                               "halda_sweep_steps_kernel): batch t reads resident copy (first + t) % copies and writes "
-                               "its results, bit-identical to its own launch; one wave per (batch, fleet) item, the "
-                               "hardware dispatcher starting the next batch's waves where the last ones end",
-                       "persistent": group.persistent, "launches_per_region": 1 if group.persistent else args.steps,
-                       "stream": 1},
-            "per_launch": {"what": "the same K steps as K launches (one per batch, halda_fleets_plan_launch_many) "
-                                   "alternating over the streams: two batches in flight",
-                           "ms_per_step": el_sweep2 / args.steps * 1e3, "instances_per_s": total / el_sweep2,
-                           "host_enqueue_ms_per_step": HOST_ENQUEUE["per_launch"] / args.steps * 1e3,
-                           "streams": args.streams},
-            "one_stream": {"what": "the same K steps as K launches all on one stream (each batch waits for the "
-                                   "previous)",
-                           "ms_per_step": el_sweep1 / args.steps * 1e3, "instances_per_s": total / el_sweep1},
-            "host_enqueue_ms_per_step": HOST_ENQUEUE["headline"] / args.steps * 1e3,
-            "feasible_instances_per_s": value * n_opt / batch.n_inst,
-            "fleets_per_s": n_fleets_total / el_sweep,
-            "time_to_optimal_ms": tto,
-            "time_to_optimal_parts": tto_parts,
             "roofline": group_roofline(group_ms, args.steps, alg["halda_sweep_kernel"], len(fleets),
                                        roofline(fl_mean, alg, pmc_traffic, sweep_ev_ms)),
+            "cpu_baseline": cpu_base,
+            "launch": {"persistent": group.persistent, "launches_per_region": 1 if group.persistent else args.steps},
+            "rank_launch_ms": rank_launch_ms,
+            "weak_200": None if el_200 is None else {"ms_per_step": el_200 / 200 * 1e3,
+                                                      "instances_per_s": inst_rank * world * 200 / el_200},
+            "per_launch": {"ms_per_step": el_sweep2 / args.steps * 1e3, "instances_per_s": total / el_sweep2,
+                           "host_enqueue_ms_per_step": HOST_ENQUEUE["per_launch"] / args.steps * 1e3,
+                           "streams": args.streams},
+            "one_stream": {"ms_per_step": el_sweep1 / args.steps * 1e3, "instances_per_s": total / el_sweep1},
+            "host_enqueue_ms_per_step": HOST_ENQUEUE["headline"] / args.steps * 1e3,
+            "strong": None if el_strong is None else {
+                "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,
+                "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
+            },
+            "latency_mode": lat,
+            "setup_s": setup_s,
+            "fleets_per_s": n_fleets_total / el_sweep,
+            "c5_stream": c5,
             "solve_only": {
-                "what": "same fleets lowered on the host beforehand, the lowering's bound-infeasible k's (M > "
-                        "L/k) passed as settled flags; halda_solve_batch_device_settled on the CSR batch "
-                        "resident in HBM (the milp() replacement alone); consecutive batches alternate over the "
-                        "streams like the headline (ms_per_step_one_stream: all on one stream; *_no_settled: "
-                        "halda_solve_batch_device, the screen proving every verdict itself)",
                 "instances_per_s": inst_rank * world * args.steps / el_solve,
                 "ms_per_step": el_solve / args.steps * 1e3,
                 "ms_per_step_one_stream": el_solve1 / args.steps * 1e3,
@@ -1006,18 +1101,16 @@ def main():
                 "resident_copies": n_so,
                 "roofline": roofline(so_mean, alg_so, pmc_traffic),
             },
-            "strong": None if el_strong is None else {
-                "fleets_total": C3_FLEETS, "ms_per_step": el_strong / args.steps * 1e3,
-                "instances_per_s": C3_FLEETS * len(ks) * args.steps / el_strong,
-            },
             "c2": c2,
-            "latency_mode": lat,
-            "c5_stream": c5,
             "batch_api": bapi,
-            "cpu_baseline": cpu_base,
-            "setup_s": setup_s,
+            "feasible_instances_per_s": value * n_opt / batch.n_inst,
+            "time_to_optimal_parts": tto_parts,
+            "time_to_optimal_ms": tto,
         }
-        print(json.dumps(line), flush=True)
+        if args.full_json:
+            Path(args.full_json).parent.mkdir(parents=True, exist_ok=True)
+            Path(args.full_json).write_text(json.dumps(full, indent=1) + "\n")
+        print(json.dumps(compact_line(full)), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One round's profile set, run on the GPU box from the repo root (build beforehand, in this tree):
-#   bash profiles/run_round.sh r05
+#   bash profiles/run_round.sh r06
 # 1) rocprofv3 kernel trace + stats of the bench (--streams 1: each dispatch's begin..end is its own)
 # 2) PMC passes, one counter group per run (MI355X_MICROARCH.md): FETCH_SIZE, WRITE_SIZE, the
 #    FETCH_SIZE calibration binary, and the SQ instruction counts of the fused-sweep kernels on C3 and
@@ -31,13 +31,20 @@ for M in 64 16; do
       --kernel-trace --output-format csv -d "$OUT/valu_m$M" -o run -- \
       python3 tools/sweep_time.py --M $M --paths fused --iters 3 > "$OUT/valu_m$M.log" 2>&1
 done
-echo "[prof] sq steps"
-timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS \
-    --kernel-trace --output-format csv -d "$OUT/valu_steps" -o run -- \
-    python3 tools/steps_profile.py --steps 20 --single 0 > "$OUT/valu_steps.log" 2>&1
-timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS \
-    --kernel-trace --output-format csv -d "$OUT/valu_steps16" -o run -- \
-    python3 tools/steps_profile.py --steps 20 --single 0 --M 16 > "$OUT/valu_steps16.log" 2>&1
+# the steps launches (the headline's and C2's): the SQ pass, then the per-type VALU pass (FP64 arithmetic
+# apart from the rest, for the VALU-issue roof's pricing; 8 SQ counters, one pass)
+TYPES="SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT"
+for M in 64 16; do
+  echo "[prof] sq steps M=$M"
+  timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS \
+      --kernel-trace --output-format csv -d "$OUT/valu_steps$M" -o run -- \
+      python3 tools/steps_profile.py --steps 20 --single 0 --M $M > "$OUT/valu_steps$M.log" 2>&1
+  echo "[prof] valu types steps M=$M"
+  timeout -s KILL 180 rocprofv3 --pmc $TYPES \
+      --kernel-trace --output-format csv -d "$OUT/types_steps$M" -o run -- \
+      python3 tools/steps_profile.py --steps 20 --single 0 --M $M > "$OUT/types_steps$M.log" 2>&1
+done
 python3 tools/valu_stamp.py "$R" c3="$OUT/valu_m64/run_counter_collection.csv" c2="$OUT/valu_m16/run_counter_collection.csv" \
-    c3_steps="$OUT/valu_steps/run_counter_collection.csv:81920" c2_steps="$OUT/valu_steps16/run_counter_collection.csv:81920" > /dev/null
+    c3_steps="$OUT/valu_steps64/run_counter_collection.csv+$OUT/types_steps64/run_counter_collection.csv:81920" \
+    c2_steps="$OUT/valu_steps16/run_counter_collection.csv+$OUT/types_steps16/run_counter_collection.csv:81920" > /dev/null
 echo "[prof] done"
