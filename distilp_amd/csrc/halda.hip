@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -79,6 +80,8 @@ struct Ctx {
     uint32_t rseq = 0;
     bool rlive = false;
     bool resident = true;  // HALDA_RESIDENT=0 at halda_init: every small call launches its own kernel
+    bool resident_drop = false;  // HALDA_RESIDENT_TEST=drop (fault injection): requests are never posted
+    std::vector<void *> retired;  // pinned buffers a resident wave that would not stop may still write
     size_t pinned_bytes = 0;
     size_t scratch_bytes = 0;
     void *work = nullptr;  // cls[n]: screen verdict per instance
@@ -146,22 +149,34 @@ struct Ctx {
     // The dynamic-LDS limit is a per-function attribute of the whole process: it only ever rises here
     // (the largest size any plan of any context asked for), so a plan made for a large slice stays
     // launchable after a smaller one was planned for the same kernel.
+    // Keyed by (device, kernel) -- contexts on several devices (halda_init_multi) each raise their own --
+    // and guarded by a lock: contexts may be driven from different host threads.
     struct LdsAttr {
+        int device;
         const void *fn;
         int64_t lds;
     };
-    static inline LdsAttr lds_attr[16] = {};
+    static constexpr int kLdsAttrs = 64;
+    static inline std::mutex lds_mu;
+    static inline LdsAttr lds_attr[kLdsAttrs] = {};
     static inline int n_lds_attr = 0;
     static hipError_t ensure_lds(const void *fn, int64_t lds) {
-        int i = 0;
-        while (i < n_lds_attr && lds_attr[i].fn != fn) ++i;
-        if (i < n_lds_attr && lds_attr[i].lds >= lds) return hipSuccess;
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
-        if (i == n_lds_attr && n_lds_attr < 16) ++n_lds_attr;
-        if (i < 16) lds_attr[i] = LdsAttr{fn, lds};
+        std::lock_guard<std::mutex> lock(lds_mu);
+        int i = 0;
+        while (i < n_lds_attr && !(lds_attr[i].fn == fn && lds_attr[i].device == dev)) ++i;
+        if (i < n_lds_attr && lds_attr[i].lds >= lds) return hipSuccess;
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        if (i == n_lds_attr && n_lds_attr < kLdsAttrs) ++n_lds_attr;
+        if (i < kLdsAttrs) lds_attr[i] = LdsAttr{dev, fn, lds};
         return hipSuccess;
     }
+    // process-unique (a freed context's address may be reused by the next one): keys the plan cache
+    static inline std::atomic<uint64_t> next_uid{1};
+    uint64_t uid = next_uid.fetch_add(1);
     std::vector<CtxHandle *> handles;  // live plans / groups made on this context
     void detach(CtxHandle *h) { handles.erase(std::remove(handles.begin(), handles.end(), h), handles.end()); }
     hipError_t occupancy(const void *fn, int64_t lds, int *per_cu) {
@@ -690,7 +705,7 @@ int cached_plan(Ctx *c, const halda_model &model, const halda_fleets &F, const i
                 const halda_fleet_result &out, SweepPlan **plan) {
     static thread_local SweepKey last_key;
     static thread_local SweepPlan last_plan;
-    static thread_local const Ctx *last_ctx = nullptr;
+    static thread_local uint64_t last_ctx = 0;  // Ctx::uid
     SweepKey k;
     std::memset(&k, 0, sizeof k);
     k.model = model;
@@ -700,12 +715,12 @@ int cached_plan(Ctx *c, const halda_model &model, const halda_fleets &F, const i
     k.n_k = n_k;
     k.path_gen = c->path_gen;
     k.x_zero = c->x_zero;
-    if (last_ctx != c || std::memcmp(&k, &last_key, sizeof k) != 0) {
-        last_ctx = nullptr;
+    if (last_ctx != c->uid || std::memcmp(&k, &last_key, sizeof k) != 0) {
+        last_ctx = 0;
         const int rc = plan_sweep(c, model, F, kh, n_k, out, &last_plan);
         if (rc != HALDA_OK) return rc;
         last_key = k;
-        last_ctx = c;
+        last_ctx = c->uid;
     }
     *plan = &last_plan;
     return HALDA_OK;
@@ -722,11 +737,30 @@ int sweep_fleets(Ctx *c, const halda_model &model, const halda_fleets &F, const 
 // One fleet through the resident wave (halda_resident_kernel), synchronously: the plan's arguments into
 // the mailbox, the wave (re)launched when no launch of it is running, seq bumped, ack awaited. The
 // fleet's table and results are the caller's fine-grained pinned buffers (device addresses in A).
-// *done = false when the plan is not a register-only sweep of one fleet (the caller launches it).
+// *done = false when the plan is not a register-only sweep of one fleet, or when the wave gave no answer
+// in time and was stopped (the caller launches the sweep itself; the resident path is off from then on).
+// *retry = true when the wave could not even be stopped: its pinned buffer is retired (kept allocated,
+// never reused) and the caller redoes the whole call on a fresh one.
 constexpr uint32_t kResidentIdleTicks = 200000;  // 2 ms of the 100 MHz clock without a request
 
-int resident_sweep(Ctx *c, const SweepPlan &p, bool *done) {
+// Stop the resident wave and wait (at most `budget`) until it has left: true when it has (or none ran).
+bool resident_stop(Ctx *c, std::chrono::milliseconds budget) {
+    if (!c->rbox || !c->rlive) return true;
+    __atomic_store_n(&c->rbox->stop, 1u, __ATOMIC_SEQ_CST);
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipEventQuery(c->rdone)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > budget) return false;
+        std::this_thread::yield();
+    }
+    c->rlive = false;
+    __atomic_store_n(&c->rbox->stop, 0u, __ATOMIC_SEQ_CST);  // the next launch stays until told
+    return true;
+}
+
+int resident_sweep(Ctx *c, const SweepPlan &p, bool *done, bool *retry) {
     *done = false;
+    *retry = false;
     if (!c->resident || p.kind != kRegAlone || p.nf != 1 || p.A.uM <= 0 || p.A.uM > kK1MaxM || p.A.k1dp) return HALDA_OK;
     if (!c->rbox) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->rbox), sizeof(ResidentBox),
@@ -760,9 +794,11 @@ int resident_sweep(Ctx *c, const SweepPlan &p, bool *done) {
         if (rc != HALDA_OK) return rc;
     }
     const uint32_t want = ++c->rseq;
-    __atomic_store_n(&box->seq, want, __ATOMIC_SEQ_CST);  // after the request (x86: stores in order)
+    // after the request (x86: stores in order); the fault-injection mode never posts it
+    if (!c->resident_drop) __atomic_store_n(&box->seq, want, __ATOMIC_SEQ_CST);
     // the answer; a wave that left (idle timeout) between its last poll and this request is relaunched
     const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = c->resident_drop ? std::chrono::milliseconds(20) : std::chrono::milliseconds(5000);
     for (uint64_t spin = 1;; ++spin) {
         if (__atomic_load_n(&box->ack, __ATOMIC_ACQUIRE) == want) break;
         if ((spin & 255) == 0) {
@@ -770,9 +806,18 @@ int resident_sweep(Ctx *c, const SweepPlan &p, bool *done) {
                 const int rc = launch(want - 1);
                 if (rc != HALDA_OK) return rc;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-                c->resident = false;  // never again on this context: back to a launch per call
-                return fail(HALDA_E_HIP, "resident solver: no answer within 5 s");
+            if (std::chrono::steady_clock::now() - t0 > limit) {
+                // no answer: never again on this context. The wave (or a late launch of it) still sees
+                // request `want` pending and would write its results into the pinned buffer later, so it
+                // is stopped and awaited before that buffer is touched again; then this call launches.
+                c->resident = false;
+                if (resident_stop(c, std::chrono::milliseconds(5000))) return HALDA_OK;
+                c->retired.push_back(c->pinned);  // still the wave's: keep it allocated, never reuse it
+                c->pinned = nullptr;
+                c->pinned_dev = nullptr;
+                c->pinned_bytes = 0;
+                *retry = true;
+                return HALDA_OK;
             }
         }
     }
@@ -1017,6 +1062,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->host_copy = hp && std::strcmp(hp, "copy") == 0;
     const char *rs = std::getenv("HALDA_RESIDENT");
     c->resident = !(rs && std::strcmp(rs, "0") == 0);
+    const char *rt = std::getenv("HALDA_RESIDENT_TEST");
+    c->resident_drop = rt && std::strcmp(rt, "drop") == 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evs) != hipSuccess || hipEventCreate(&c->evk) != hipSuccess ||
@@ -1028,6 +1075,14 @@ int halda_init(int device_ordinal, void **ctx_out) {
         return fail(HALDA_E_HIP, "stream/event creation failed");
     }
     *ctx_out = c;
+    return HALDA_OK;
+}
+
+int halda_resident_release(void *ctx) {
+    Ctx *c = static_cast<Ctx *>(ctx);
+    if (!c) return fail(HALDA_E_ARG, "null context");
+    if (!resident_stop(c, std::chrono::milliseconds(5000)))
+        return fail(HALDA_E_HIP, "resident solver: the wave did not leave within 5 s");
     return HALDA_OK;
 }
 
@@ -1043,6 +1098,7 @@ void halda_free(void *ctx) {
         }
         (void)hipHostFree(c->rbox);
     }
+    for (void *b : c->retired) (void)hipHostFree(b);  // the wave that held them has left (above)
     if (c->rdone) (void)hipEventDestroy(c->rdone);
     if (c->rstream) (void)hipStreamDestroy(c->rstream);
     (void)hipSetDevice(c->device);
@@ -1744,12 +1800,12 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
             return rc0;
         }
         SweepPlan *p = nullptr;
+        bool retry = false;
         int rc1 = cached_plan(c, *model, d, ks, n_k, r, &p);
-        if (rc1 == HALDA_OK) rc1 = resident_sweep(c, *p, &resident);
-        if (rc1 != HALDA_OK) {
-            c->x_zero = true;
-            return rc1;
-        }
+        if (rc1 == HALDA_OK) rc1 = resident_sweep(c, *p, &resident, &retry);
+        c->x_zero = rc1 != HALDA_OK || retry ? true : c->x_zero;
+        if (rc1 != HALDA_OK) return rc1;
+        if (retry) return halda_solve_fleets_host(ctx, model, fh, ks, n_k, out_h);  // on a fresh pinned buffer
     }
     const int rc = resident ? HALDA_OK : halda_solve_fleets(ctx, model, &d, ks, n_k, &r, s);
     c->x_zero = true;

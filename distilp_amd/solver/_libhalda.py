@@ -84,7 +84,8 @@ EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batc
            "halda_free_multi", "halda_comm_unique_id", "halda_comm_init", "halda_comm_destroy",
            "halda_solve_fleets_sharded", "halda_fleets_plan_create", "halda_fleets_plan_launch",
            "halda_fleets_plan_free", "halda_solve_fleets_sharded_emulated", "halda_fleets_plan_launch_many",
-           "halda_fleets_group_create", "halda_fleets_group_launch", "halda_fleets_group_free")
+           "halda_fleets_group_create", "halda_fleets_group_launch", "halda_fleets_group_free",
+           "halda_resident_release")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -152,6 +153,8 @@ def load_library(path: Path | str | None = None):
         lib.halda_last_error.restype = ctypes.c_int
         lib.halda_free.argtypes = [ctypes.c_void_p]
         lib.halda_free.restype = None
+        lib.halda_resident_release.argtypes = [ctypes.c_void_p]
+        lib.halda_resident_release.restype = ctypes.c_int
         if path is None:
             _lib = lib
         return lib
@@ -232,6 +235,14 @@ class HaldaContext:
         if getattr(self, "ctx", None):
             self.lib.halda_free(self.ctx)
             self.ctx = None
+
+    def release_resident(self):
+        """Let the context's resident single-fleet wave go now (halda_resident_release) instead of after
+        its 2 ms idle limit: for a caller about to wait on the whole device through libhalda's runtime."""
+        with self._lock:
+            rc = self.lib.halda_resident_release(self.ctx)
+        if rc != 0:
+            raise RuntimeError(f"halda_resident_release failed ({rc}): {last_error(self.lib)}")
 
     def __del__(self):  # pragma: no cover - interpreter shutdown order
         try:

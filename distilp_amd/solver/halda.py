@@ -133,6 +133,8 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                 # views of the rows (the workspace is read before this thread's next call): c.dot(x) is
                 # numpy's 1-D dot on the same contiguous rows, the reference's float(c @ x) bits
                 q = xrow[j]  # an optimal k has L // k >= M (each device takes a layer): its row came back
+                if q < 0:  # never another k's row (w >= 1 bounds today, halda_p_solver.py:117)
+                    raise RuntimeError(f"libhalda returned k={k} optimal without its x / c row (L // k < M)")
                 x = X[q, :N]
                 obj = float(C[q, :N].dot(x)) + t_comm + xi_sum + kappa
                 wn = np.rint(x[:2 * M]).astype(np.int64).tolist()  # int(round(v)): both round half to even

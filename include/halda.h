@@ -281,9 +281,16 @@ int halda_set_fleets_path(void *ctx, int path);
 int halda_last_fleet_ms(void *ctx, double *ms8);
 
 /* Synchronous variant on HOST arrays (halda_fleets / halda_fleet_result in host
- * memory; obj_by_k and status may be NULL). */
+ * memory; obj_by_k and status may be NULL). A one-fleet call (a single halda_solve) is answered by a
+ * wave the context keeps resident on its own stream: it stays for up to 2 ms after each answer (or
+ * until halda_resident_release / halda_free), and any device-wide wait of libhalda's HIP runtime
+ * (hipDeviceSynchronize, hipFree) in that window waits for it. */
 int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fleets, const int32_t *ks,
                             int32_t n_k, halda_fleet_result *out);
+
+/* Ask the context's resident wave (above) to leave now and wait until it has (a no-op when none
+ * runs); the next one-fleet call relaunches it. For callers about to synchronise the whole device. */
+int halda_resident_release(void *ctx);
 
 /* Several GPUs from one process: a context per device (ordinals may repeat), and
  * halda_solve_fleets_host over all of them -- the fleets are dealt out in contiguous blocks, one host

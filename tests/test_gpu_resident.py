@@ -98,3 +98,48 @@ def test_context_with_a_resident_wave_is_freed_promptly(llama_online_model):
     t0 = time.perf_counter()
     ctx.close()
     assert time.perf_counter() - t0 < 1.0
+
+
+def test_resident_timeout_stops_the_wave_and_launches(llama_online_model, launch_ctx):
+    """A resident wave that gives no answer in time (fault injection: HALDA_RESIDENT_TEST=drop never posts
+    the request, so the wave idles while the host waits 20 ms): the call stops the wave, waits until it
+    has left -- so it can never write a stale answer into the pinned buffer later -- and answers by a
+    launch instead of failing; the context keeps working (launch per call from then on), bit for bit."""
+    os.environ["HALDA_RESIDENT_TEST"] = "drop"
+    try:
+        ctx = HaldaContext(0)
+    finally:
+        os.environ.pop("HALDA_RESIDENT_TEST", None)
+    try:
+        ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+        for i, M in enumerate((64, 17, 64, 3)):
+            table = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(42000 + i, M)]],
+                                llama_online_model)
+            got = _call(ctx, table, llama_online_model, ks)
+            want = _call(launch_ctx, table, llama_online_model, ks)
+            for k in want:
+                assert np.array_equal(got[k], want[k]), (i, M, k)
+    finally:
+        t0 = time.perf_counter()
+        ctx.close()
+        assert time.perf_counter() - t0 < 1.0
+
+
+def test_resident_release_lets_the_wave_go_at_once(llama_online_model, launch_ctx):
+    """halda_resident_release right after a resident call returns within a fraction of the wave's 2 ms idle
+    limit (it stops the wave instead of waiting it out), is a no-op when repeated, and the next call
+    relaunches the wave with the same answers."""
+    ctx = get_context(0)
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    table = fleet_table([[DeviceProfile.model_validate(d) for d in synth_fleet(43000, 64)]], llama_online_model)
+    want = _call(launch_ctx, table, llama_online_model, ks)
+    took = []
+    for _ in range(5):
+        got = _call(ctx, table, llama_online_model, ks)
+        for k in want:
+            assert np.array_equal(got[k], want[k]), k
+        t0 = time.perf_counter()
+        ctx.release_resident()
+        took.append(time.perf_counter() - t0)
+        ctx.release_resident()  # nothing resident now
+    assert sorted(took)[2] < 1.5e-3, took
