@@ -99,6 +99,8 @@ struct Ctx {
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     int kslot_split = 2;                         // k-slot launch: the longest scan split over 2 waves (0: unsplit)
     bool kslot_opt = true;                       // ... its part 1 optimistic (leaf checks / phase 0 by other waves)
+    int kslot_pad = 0;                           // HALDA_KSLOT_LDS_PAD (diagnostic): unused LDS bytes per
+                                                 // k-slot workgroup, to measure the occupancy's effect
     int kslot_crit_w4 = 8;                       // k-slot table share of the critical slot's wave (quarters; 2x:
                                                  // measured best of 7..12 since part 1 leaves its leaf checks and
                                                  // phase 0 to other waves; 2.5x before)
@@ -456,9 +458,10 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
         const int q = SA.n_slot++;
         SA.j[q] = j;
         SA.r1[q] = W - F.min_devices + 1;
-        SA.tab[q] = kh[j] > 1 && W > F.min_devices ? mmax * SA.r1[q] + mmax : 0;
+        // a fleet of M >= min_devices devices has R + 1 <= r1 rows of odd stride <= odd_stride(r1)
+        SA.tab[q] = kh[j] > 1 && W > F.min_devices ? mmax * odd_stride(SA.r1[q]) : 0;
         SA.off[q] = int(kslot_lds);
-        kslot_lds += (64 / kSegLanes) * seg_slice_bytes(mmax, SA.tab[q]);
+        kslot_lds += (64 / kSegLanes) * kslot_slice_bytes(mmax, SA.tab[q]);
     }
     bool kslot_all = true;  // every k that is open for some fleet has a slot
     for (int j = 0, q = 0; j < n_k; ++j) {
@@ -467,8 +470,12 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
         kslot_all = kslot_all && q < SA.n_slot && SA.j[q] == j;
         ++q;
     }
-    SA.pick_off = int(kslot_lds);
-    kslot_lds += int64_t(64 / kSegLanes) * SA.n_slot * int64_t(sizeof(SlotPick));
+    // region 0 holds, one after another, the device records (read before any table is written), the
+    // tables, and the pick area (written after the last table read): as large as the largest of them
+    const int64_t pick_bytes = int64_t(64 / kSegLanes) * SA.n_slot * int64_t(sizeof(SlotPick));
+    kslot_lds = std::max<int64_t>({kslot_lds, pick_bytes, int64_t(sizeof(KslotRecs))});
+    SA.pick_off = 0;
+    SA.rec_off = 0;
     // the threshold scan of the slot with the largest tables (C2: k = 2, the workgroup's critical path)
     // is split over kslot_split waves: the slot's own and, first thing after the tables, the waves of
     // the lightest other slots (no tables: k = 1 / W = M; else the smallest tables) -- an extra wave
@@ -528,8 +535,7 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
     SA.split_off = int(kslot_lds);
     if (SA.helper >= 0) kslot_lds += int64_t(64 / kSegLanes) * int64_t(sizeof(SplitArea));
     kslot_lds = align16(kslot_lds);
-    SA.rec_off = int(kslot_lds);
-    kslot_lds += int64_t(sizeof(KslotRecs));
+    kslot_lds += c->kslot_pad;
     const bool kslot = c->seg_sweep && c->kslot_sweep && fits && mmax <= kSegLanes && tab_kc > 0 && kslot_all &&
                        SA.n_slot >= 1 && nf > kSweepSmallBatch && kslot_lds <= kLdsBudget;
     const bool seg = !kslot && c->seg_sweep && fits && mmax <= kSegLanes && n_k <= kSegLanes && tab_kc > 0 &&
@@ -615,7 +621,19 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
                 1, std::min<int64_t>({int64_t(c->cus) * per_cu, int64_t(nf), kGlobalTableBudget / A.gstride})));
         }
     }
-    if (p.kind == kKslotGated) HIP_TRY(c->occupancy(p.fn1, p.lds, nullptr));
+    if (p.kind == kKslotGated) {
+        int per_cu = 0;
+        HIP_TRY(c->occupancy(p.fn1, p.lds, &per_cu));
+        if (std::getenv("HALDA_DEBUG_PLAN")) {  // diagnostic: the k-slot launch's LDS and residency
+            int steps_cu = 0;
+            (void)c->ensure_lds(reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel), p.lds);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &steps_cu, reinterpret_cast<const void *>(halda_sweep_kslot_steps_kernel), int(p.block1),
+                size_t(p.lds));
+            std::fprintf(stderr, "halda plan: k-slot lds %lld B, block %u, per CU %d (steps kernel %d)\n",
+                         (long long)p.lds, p.block1, per_cu, steps_cu);
+        }
+    }
     if (p.kind == kKslotGated || p.kind == kSegGated)
         HIP_TRY(c->occupancy(reinterpret_cast<const void *>(halda_sweep_tables_kernel), slice, nullptr));
     return HALDA_OK;
@@ -1062,6 +1080,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->host_copy = hp && std::strcmp(hp, "copy") == 0;
     const char *rs = std::getenv("HALDA_RESIDENT");
     c->resident = !(rs && std::strcmp(rs, "0") == 0);
+    const char *kp = std::getenv("HALDA_KSLOT_LDS_PAD");
+    c->kslot_pad = kp ? std::max(0, std::atoi(kp)) : 0;
     const char *rt = std::getenv("HALDA_RESIDENT_TEST");
     c->resident_drop = rt && std::strcmp(rt, "drop") == 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||

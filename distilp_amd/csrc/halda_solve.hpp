@@ -1022,7 +1022,7 @@ struct SplitArea {  // per segment, in LDS
     int lo_sum, capsum;
     int pub;             // 0: not yet, 1: published, 2: part 1 does not scan (the helpers skip)
     int verdict;         // the helper's leaf check of part 1's rows (optimistic part 1): 0 not yet, 1 ok, 2 not
-    int lo[16], hi[16];  // each device's finite leaf range
+    int16_t lo[16], hi[16];  // each device's finite leaf range (R + 1 < 2^15: a split slot's tables fit LDS)
     // the helpers -> part 1
     double alt_best[kMaxSplitParts - 1];  // part p's best objective (+inf: nothing beat its start)
     int flag[kMaxSplitParts - 1];         // set once part p's alt_e / alt_best are final

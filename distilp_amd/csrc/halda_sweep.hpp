@@ -1309,25 +1309,31 @@ __global__ __launch_bounds__(64, HALDA_SEG_WAVES_PER_SIMD) void halda_sweep_seg_
 constexpr int kMaxSlots = 16;
 constexpr int kSlotFlagged = 1000;  // SlotPick.st: the fleet goes to the table launch
 
-struct SlotPick {  // one (segment, k-slot) result in the workgroup's pick area
-    double obj;    // obj_value when OPTIMAL, else +inf
-    int st;        // HALDA_STATUS_* or kSlotFlagged
+struct SlotPick {  // one (segment, k-slot) result in the workgroup's pick area (written after the last use of the
+    double obj;    // tables, over them); the slot's (w, n) stay in its wave's registers, and the winning wave
+    int st;        // writes them (kslot_pick). st: HALDA_STATUS_* or kSlotFlagged
     int pad;
-    int w[kSegLanes], n[kSegLanes];
 };
+
+// LDS bytes of one segment's slice of a k-slot (none for a slot without tables: the k = 1 greedy and the
+// forced W = M split run in registers).
+__host__ __device__ inline int64_t kslot_slice_bytes(int mmax, int tab) {
+    return tab > 0 ? seg_slice_bytes(mmax, tab) : 0;
+}
 
 struct SlotArgs {
     int n_slot;
-    int pick_off;              // LDS byte offset of the pick area (SlotPick [4][n_slot])
+    int pick_off;              // LDS byte offset of the pick area (SlotPick [4][n_slot]; over the tables, dead by then)
     int j[kMaxSlots];          // k index of slot q (ascending)
-    int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * (R + 1) + max_devices, 0: no tables
+    int tab[kMaxSlots];        // doubles of G (and of H) per segment: max_devices * odd_stride(R + 1), 0: no tables
     int r1[kMaxSlots];         // largest R + 1 of slot q over the batch
     int off[kMaxSlots];        // LDS byte offset of slot q's four segment slices
     int helper;                // slot whose threshold scan is split over n_parts waves (-1: none)
     int n_parts;               // 2 (split) or 0
     int part_wave[kMaxSplitParts - 1];  // the wave that takes part 2 first: a light slot's, or n_slot
     int split_off;             // LDS byte offset of the split areas (SplitArea [4])
-    int rec_off;               // LDS byte offset of the workgroup's device records (KslotRecs)
+    int rec_off;               // LDS byte offset of the workgroup's device records (KslotRecs; over the tables,
+                               // which are written only after every wave has read its records)
     int check_wave;            // the wave that checks the split slot's leaves after its own slot (-1: none)
     int opt;                   // 1: an optimistic part 1 where its rows allow (0: the sequential order, a test path)
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
@@ -1425,7 +1431,7 @@ __device__ inline bool kslot_uses_tables(const KslotFleet &fd, int k, int W, int
 __device__ inline WaveCtx kslot_ctx(const SweepArgs &A, const SlotArgs &SA, int p, unsigned char *smem, int seg) {
     const int tab = SA.tab[p];
     const int64_t tb = align16(int64_t(tab) * 8);
-    unsigned char *base = smem + SA.off[p] + int64_t(seg) * seg_slice_bytes(A.mmax, tab);
+    unsigned char *base = smem + SA.off[p] + int64_t(seg) * kslot_slice_bytes(A.mmax, tab);
     WaveCtx w = {};
     w.G = reinterpret_cast<double *>(base);
     w.H = reinterpret_cast<double *>(base + tb);
@@ -1479,8 +1485,8 @@ __device__ void kslot_tables(const SweepArgs &A, const SlotArgs &SA, int q, int 
 }
 
 __device__ void sweep_kslot(const SweepArgs &A, const SweepBatch &B, const KslotFleet &fd, int f, int j, int r1cap,
-                            int tabcap, const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick *pk,
-                            unsigned long long *t_rec, const ScanSplit sp) {
+                            int tabcap, const WaveCtx &w, const Seg<kSegLanes> &sg, SlotPick &pk,
+                            unsigned long long *t_rec, const ScanSplit sp, int &wl, int &nl) {
     using SG = Seg<kSegLanes>;
     constexpr int S = SG::S;
     const int lane = sg.sl;
@@ -1496,7 +1502,8 @@ __device__ void sweep_kslot(const SweepArgs &A, const SweepBatch &B, const Kslot
     const double kc = double(k - 1);
     int st;
     double obj = kInf;
-    int wl = 0, nl = 0;  // this lane's (w, n) in the solution
+    wl = 0;  // this lane's (w, n) in the solution
+    nl = 0;
     if (!(W < 1000000)) st = HALDA_STATUS_UNSUPPORTED;
     else if (M > W) st = HALDA_STATUS_INFEASIBLE;  // sum lb(w) = M > W (HiGHS presolve)
     else if (anybad) st = HALDA_STATUS_UNSUPPORTED;
@@ -1609,20 +1616,16 @@ __device__ void sweep_kslot(const SweepArgs &A, const SweepBatch &B, const Kslot
                 }
         }
     }
-    if (lane == 0) {
-        pk->obj = st == HALDA_STATUS_OPTIMAL ? obj : kInf;
-        pk->st = st;
-    }
-    if (lane < M) {
-        pk->w[lane] = wl;
-        pk->n[lane] = nl;
-    }
+    pk.obj = st == HALDA_STATUS_OPTIMAL ? obj : kInf;  // (lane 0's are the segment's)
+    pk.st = st;
 }
 
-// The pick of one fleet (segment lanes): best k over the slots in ascending k with strict "<", the
-// settled k's of no slot, best_k / obj_value / w / n and the fleet's flag byte.
+// The pick of one fleet (segment lanes), run by every slot wave q after the last barrier: best k over the
+// slots in ascending k with strict "<"; the winning slot's wave writes its (w, n) from its registers (wl,
+// nl), wave 0 the settled k's of no slot, best_k / obj_value, the fleet's flag byte and, when no k is
+// feasible, zero (w, n).
 __device__ void kslot_pick(const SweepArgs &A, const SweepBatch &B, const SlotArgs &SA, int f, const SlotPick *pk,
-                           const Seg<kSegLanes> &sg) {
+                           const Seg<kSegLanes> &sg, int q, int wl, int nl) {
     constexpr int S = kSegLanes;
     const int lane = sg.sl;
     const int64_t d0 = A.uM > 0 ? int64_t(f) * A.uM + B.F.dev_off[0] : B.F.dev_off[f];
@@ -1639,6 +1642,11 @@ __device__ void kslot_pick(const SweepArgs &A, const SweepBatch &B, const SlotAr
         }
     }
     if (flagged) return;  // the table launch redoes this fleet (fflag / hb_flag set by the slot wave)
+    if (q == bq && lane < M) {
+        B.out.w[d0 + lane] = wl;
+        B.out.n[d0 + lane] = nl;
+    }
+    if (q != 0) return;
     // k's of no slot: settled for every fleet of the batch (W >= 1e6 unsupported, else M > W)
     for (int jj = lane; jj < A.n_k; jj += S) {
         bool slot = false;
@@ -1662,9 +1670,9 @@ __device__ void kslot_pick(const SweepArgs &A, const SweepBatch &B, const SlotAr
         B.out.obj_value[f] = best;
         B.fflag[f] = 0;
     }
-    if (lane < M) {
-        B.out.w[d0 + lane] = bq >= 0 ? pk[bq].w[lane] : 0;
-        B.out.n[d0 + lane] = bq >= 0 ? pk[bq].n[lane] : 0;
+    if (bq < 0 && lane < M) {
+        B.out.w[d0 + lane] = 0;
+        B.out.n[d0 + lane] = 0;
     }
 }
 
@@ -1810,6 +1818,7 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         }
         __syncthreads();  // the records are in LDS
         if (q != 0 && f < nf) fd = kslot_get_records(A, B.F, recs, int(f), lane, seg);
+        __syncthreads();  // every wave has its records: the tables below may overwrite them
         HALDA_KSTAMPW(1, __builtin_amdgcn_s_memtime());
         if (f < nf) kslot_tables(A, SA, q, crit, fd, sg, smem, seg);
         const int my_part = kslot_part_of(SA, q);
@@ -1825,7 +1834,8 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
             __builtin_amdgcn_s_setprio(3);
             if (q == SA.check_wave) kslot_check(A, SA, fd, split, sg, smem, seg, f < nf);
             kslot_helper(A, SA, fd, split, my_part, sg, smem, seg, f < nf);
-            __syncthreads();  // the pick barrier below
+            __syncthreads();  // the pick barriers below
+            __syncthreads();
             return;
         }
         const WaveCtx w = kslot_ctx(A, SA, q, smem, seg);
@@ -1840,6 +1850,8 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         }
 #endif
         unsigned long long t_rec[6] = {0, 0, 0, 0, 0, 0};
+        int wl = 0, nl = 0;
+        SlotPick mine = {kInf, HALDA_STATUS_INFEASIBLE, 0};
 #ifdef HALDA_STAMPS
         const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0,
                            int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
@@ -1849,7 +1861,7 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0};
 #endif
         if (f < nf)
-            sweep_kslot(A, B, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, pick + seg * SA.n_slot + q, t_rec, sp);
+            sweep_kslot(A, B, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, mine, t_rec, sp, wl, nl);
         if (q == SA.helper && f < nf && sg.sl == 0 && split->pub == 0) split->pub = 2;  // did not scan: helpers skip
         if (q == SA.check_wave) kslot_check(A, SA, fd, split, sg, smem, seg, f < nf);
         if (my_part) {  // after its own slot, at the split slot's priority
@@ -1860,12 +1872,14 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         HALDA_KSTAMPW(8, t_rec[3]);
         HALDA_KSTAMPW(9, t_rec[4]);
         HALDA_KSTAMPW(10, t_rec[5]);
+        HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
+        __syncthreads();  // every table read is done: the pick area over them is free
+        if (f < nf && sg.sl == 0) pick[seg * SA.n_slot + q] = mine;
+        __syncthreads();
+        HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
+        if (f < nf) kslot_pick(A, B, SA, int(f), pick + seg * SA.n_slot, sg, q, wl, nl);
+        HALDA_KSTAMPW(4, __builtin_amdgcn_s_memtime());
     }
-    HALDA_KSTAMPW(2, __builtin_amdgcn_s_memtime());
-    __syncthreads();
-    HALDA_KSTAMPW(3, __builtin_amdgcn_s_memtime());
-    if (q == 0 && f < nf) kslot_pick(A, B, SA, int(f), pick + seg * SA.n_slot, sg);
-    HALDA_KSTAMPW(4, __builtin_amdgcn_s_memtime());
 }
 
 __global__ __launch_bounds__(64 * kMaxSlots) void halda_sweep_kslot_kernel(SweepArgs A, SlotArgs SA) {

@@ -18,7 +18,10 @@ def main():
     ap.add_argument("--groups", type=int, default=3)
     ap.add_argument("--single", type=int, default=20)
     ap.add_argument("--M", type=int, default=64)
+    ap.add_argument("--ks", type=str, default="", help="comma-separated k-candidates instead of L = 80's")
+    ap.add_argument("--path", type=str, default="", help="HaldaContext.set_fleets_path name (test paths)")
     a = ap.parse_args()
+    ks = [int(k) for k in a.ks.split(",")] if a.ks else KS
     import torch
 
     import bench
@@ -28,10 +31,12 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = get_context(0)
     ctx.set_timing(False)
+    if a.path:
+        ctx.set_fleets_path(a.path)
     s = torch.cuda.Stream(dev)
     model = bench.load_model()
     table = fleet_table(bench.build_fleets(range(4096), a.M), model)
-    dts = [DeviceFleetTable(table, model, KS, 0.5, dev) for _ in range(16)]
+    dts = [DeviceFleetTable(table, model, ks, 0.5, dev) for _ in range(16)]
     group = PlanGroup(dts, ctx)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {"steps": a.steps, "persistent": group.persistent, "group_us": [], "single_us": None}
