@@ -601,7 +601,10 @@ static PyObject *int_list(const double *v, Py_ssize_t M) {
     PyObject *l = PyList_New(M);
     if (!l) return NULL;
     for (Py_ssize_t i = 0; i < M; ++i) {
-        PyObject *o = PyLong_FromDouble(nearbyint(v[i]));
+        /* the int of the rounded double (int(round(x)), half to even); a layer count is a small int,
+         * which PyLong_FromLong takes from the interpreter's cache, no allocation */
+        const double r = nearbyint(v[i]);
+        PyObject *o = fabs(r) < 9.0e18 ? PyLong_FromLongLong((long long)r) : PyLong_FromDouble(r);
         if (!o) { Py_DECREF(l); return NULL; }
         PyList_SET_ITEM(l, i, o);
     }
@@ -695,11 +698,16 @@ static PyObject *results(PyObject *self, PyObject *args) {
     Py_buffer bx, br, bk, bo, boff, bc;
     if (!PyArg_ParseTuple(args, "Oy*y*y*y*y*y*", &cls, &bx, &br, &bk, &bo, &boff, &bc)) return NULL;
     PyObject *ret = NULL, *noargs = NULL;
+    int gc_was = 0;
     const Py_ssize_t nf = br.len / 8, nx = bx.len / 8, nd = bc.len;
     if (!PyType_Check(cls) || bk.len < 8 * nf || bo.len < 8 * nf || boff.len < 8 * (nf + 1)) {
         PyErr_SetString(PyExc_ValueError, "results: bad arguments");
         goto done;
     }
+    /* the cyclic GC paused while the results are made: a few container objects per fleet would trigger
+     * collections that walk every object the caller holds (a batch's 262,144 DeviceProfile objects and
+     * their dicts: one full collection costs more than building all 4,096 results) */
+    gc_was = PyGC_Disable();
     if (!(noargs = PyTuple_New(0)) || !(ret = PyList_New(nf))) goto done;
     const double *x = (const double *)bx.buf, *obj = (const double *)bo.buf;
     const int64_t *row = (const int64_t *)br.buf, *kk = (const int64_t *)bk.buf, *off = (const int64_t *)boff.buf;
@@ -721,6 +729,7 @@ static PyObject *results(PyObject *self, PyObject *args) {
         PyList_SET_ITEM(ret, f, o);
     }
 done:
+    if (gc_was) PyGC_Enable();
     Py_XDECREF(noargs);
     PyBuffer_Release(&bx);
     PyBuffer_Release(&br);

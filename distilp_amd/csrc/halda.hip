@@ -1080,6 +1080,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->host_copy = hp && std::strcmp(hp, "copy") == 0;
     const char *rs = std::getenv("HALDA_RESIDENT");
     c->resident = !(rs && std::strcmp(rs, "0") == 0);
+    const char *kw = std::getenv("HALDA_KSLOT_CRIT_W4");  // diagnostic A/B of the critical slot's table share
+    if (kw && std::atoi(kw) > 0) c->kslot_crit_w4 = std::atoi(kw);
     const char *kp = std::getenv("HALDA_KSLOT_LDS_PAD");
     c->kslot_pad = kp ? std::max(0, std::atoi(kp)) : 0;
     const char *rt = std::getenv("HALDA_RESIDENT_TEST");

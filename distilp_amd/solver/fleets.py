@@ -233,20 +233,40 @@ def _load_packer():
 _PACKER = _load_packer()
 
 
-def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile) -> FleetTable:
+_TLS = threading.local()
+
+
+def _scratch(kind: str, shapes) -> tuple:
+    """The calling thread's reusable arrays for `kind` ((shape, dtype) each), kept between calls while the
+    shapes repeat: a batch of 4,096 C3 fleets needs ~33 MB of table and ~30 MB of results, whose first
+    touch of fresh pages costs more than the pass that fills them. One set per kind and thread."""
+    ws = getattr(_TLS, "scratch", None)
+    if ws is None:
+        ws = _TLS.scratch = {}
+    key = tuple((tuple(np.atleast_1d(sh).tolist()), np.dtype(dt).str) for sh, dt in shapes)
+    hit = ws.get(kind)
+    if hit is None or hit[0] != key:
+        hit = ws[kind] = (key, tuple(np.empty(sh, dt) for sh, dt in shapes))
+    return hit[1]
+
+
+def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile, _reuse: bool = False) -> FleetTable:
     """Pack fleets (lists of DeviceProfile) into a FleetTable: one pass of the C packer over the
     devices into three field blocks (f64 [10][nd], int64 [6][nd], uint8 [2][nd]); the table's fields
-    are rows of those blocks. Same values, flags and exceptions as fleet_table_py."""
+    are rows of those blocks. Same values, flags and exceptions as fleet_table_py. `_reuse` (internal
+    callers that are done with the table before their next call on this thread): the blocks are the
+    thread's workspace, overwritten by the next such call."""
     if _PACKER is None:  # the C packer is not built for this interpreter: the Python packer (same table)
         return fleet_table_py(fleets, model)
     fleets = fleets if isinstance(fleets, (list, tuple)) else list(fleets)
     nf = len(fleets)
     nd = sum(len(d) for d in fleets)
-    f64 = np.empty((len(F64_FIELDS), nd), np.float64)
-    b64 = np.empty((len(BYTE_FIELDS), nd), np.float64)
-    u8 = np.empty((2, nd), np.uint8)
-    off = np.empty(nf + 1, np.int64)
-    heads = np.empty(nf, np.int64)
+    shapes = (((len(F64_FIELDS), nd), np.float64), ((len(BYTE_FIELDS), nd), np.float64), ((2, nd), np.uint8),
+              (nf + 1, np.int64), (nf, np.int64))
+    if _reuse:
+        f64, b64, u8, off, heads = _scratch("table", shapes)
+    else:
+        f64, b64, u8, off, heads = (np.empty(sh, dt) for sh, dt in shapes)
     _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, b64, u8, off, heads)
     # the dataclass's fields set directly (no per-field __setattr__), then the packed blocks they view
     t = object.__new__(FleetTable)
@@ -544,7 +564,6 @@ class _OneFleet:
                                      pF + 8 * (o2 + no * xs), self.x_off.ctypes.data)
 
 
-_TLS = threading.local()
 
 
 def pack_one(devs: Sequence[DeviceProfile], model: ModelProfile, ks: Sequence[int]) -> "_OneFleet":
@@ -583,10 +602,13 @@ def sweep_one(ws: "_OneFleet", model: ModelProfile, kv_factor: float, device: in
 
 
 def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_factor: float,
-                device: int = 0, want_x: bool = False, _multi: Optional["MultiDeviceContext"] = None) -> FleetSolve:
+                device: int = 0, want_x: bool = False, _multi: Optional["MultiDeviceContext"] = None,
+                _reuse: bool = False) -> FleetSolve:
     """halda_solve_fleets_host on a host FleetTable (synchronous). want_x: also x and the lowered c
     of every (fleet, k) (so the host can form obj_value exactly as the reference, with NumPy);
-    want_x="open": only of the instances that can be optimal (open_x_offsets), flat, with x_off."""
+    want_x="open": only of the instances that can be optimal (open_x_offsets), flat, with x_off.
+    `_reuse`: the result arrays are the thread's workspace (fleet_table), overwritten by the next such
+    call; the library writes every entry of them."""
     ks = [int(k) for k in ks]
     if not ks:
         raise ValueError("no k-candidates")
@@ -604,8 +626,11 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
     else:
         xs = 7 * int(fs.max_devices) + 1 if want_x else 0
         ext = nf * nk * xs
-    fbuf = np.zeros(nf + nf * nk + 2 * ext)
-    ibuf = np.zeros(nf + 2 * nd + nf * nk, np.int32)
+    if _reuse:
+        fbuf, ibuf = _scratch("solve", ((nf + nf * nk + 2 * ext, np.float64), (nf + 2 * nd + nf * nk, np.int32)))
+    else:
+        fbuf = np.zeros(nf + nf * nk + 2 * ext)
+        ibuf = np.zeros(nf + 2 * nd + nf * nk, np.int32)
     pf, pi = fbuf.ctypes.data, ibuf.ctypes.data
     o1, o2 = nf, nf + nf * nk
     out = FleetSolve(best_k=ibuf[:nf], obj_value=fbuf[:nf], w=ibuf[nf:nf + nd], n=ibuf[nf + nd:nf + 2 * nd],

@@ -203,10 +203,12 @@ def _batch_on_gpu(fleets: Sequence[List[DeviceProfile]], model: ModelProfile, Ks
     if not fleets:
         return []
     pos = [k for k in Ks if k > 0]  # k < 0: W < 0, HiGHS reports infeasible
-    table = fleet_table(fleets, model)
+    # the table and the results are this thread's reusable workspace: everything returned is built from
+    # them below (Python ints / floats), nothing keeps a view
+    table = fleet_table(fleets, model, _reuse=True)
     if not pos:
         return [None] * len(fleets)
-    res = solve_table(table, model, pos, kv_factor, device, want_x="open", _multi=_multi)
+    res = solve_table(table, model, pos, kv_factor, device, want_x="open", _multi=_multi, _reuse=True)
     st = res.status
     bad = (st != STATUS_OPTIMAL) & (st != STATUS_INFEASIBLE)
     if bad.any():
