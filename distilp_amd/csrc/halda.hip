@@ -99,6 +99,8 @@ struct Ctx {
     bool kslot_sweep = true;                     // fused sweep: k-slot launch where it applies (else segment)
     int kslot_split = 2;                         // k-slot launch: the longest scan split over 2 waves (0: unsplit)
     bool kslot_opt = true;                       // ... its part 1 optimistic (leaf checks / phase 0 by other waves)
+    int kslot_cut8 = 4;                          // k-slot split scan's cut, eighths (HALDA_KSLOT_CUT8, A/B;
+                                                 // 4/8 since five workgroups share a CU: 5/8 before)
     int kslot_pad = 0;                           // HALDA_KSLOT_LDS_PAD (diagnostic): unused LDS bytes per
                                                  // k-slot workgroup, to measure the occupancy's effect
     int kslot_crit_w4 = 8;                       // k-slot table share of the critical slot's wave (quarters; 2x:
@@ -530,6 +532,7 @@ int plan_sweep(Ctx *c, const halda_model &model, const halda_fleets &F, const in
         }
     }
     SA.crit_w4 = c->kslot_crit_w4;
+    SA.cut8 = c->kslot_cut8;
     SA.opt = c->kslot_opt ? 1 : 0;
     kslot_lds = align16(kslot_lds);
     SA.split_off = int(kslot_lds);
@@ -1082,6 +1085,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->resident = !(rs && std::strcmp(rs, "0") == 0);
     const char *kw = std::getenv("HALDA_KSLOT_CRIT_W4");  // diagnostic A/B of the critical slot's table share
     if (kw && std::atoi(kw) > 0) c->kslot_crit_w4 = std::atoi(kw);
+    const char *kc8 = std::getenv("HALDA_KSLOT_CUT8");  // diagnostic A/B of the split scan's cut
+    if (kc8 && std::atoi(kc8) >= 1 && std::atoi(kc8) <= 7) c->kslot_cut8 = std::atoi(kc8);
     const char *kp = std::getenv("HALDA_KSLOT_LDS_PAD");
     c->kslot_pad = kp ? std::max(0, std::atoi(kp)) : 0;
     const char *rt = std::getenv("HALDA_RESIDENT_TEST");

@@ -1005,7 +1005,7 @@ __device__ void table_pass(const Src &src, const WaveCtx &w, const Inst &I, int 
 //
 // Split over two waves of a k-slot workgroup (16-lane segments only, sp.part != 0): the scan's length
 // is the workgroup's critical path, and each event is a dependent chain of reductions, so the
-// candidate range is cut at T_a (the value of rank 5/8 among the devices' H at cap(T0) + 2;
+// candidate range is cut at T_a (the value of rank 4/8 among the devices' H at cap(T0) + 2;
 // tools/scan_model.py on dumped C2 tables: the longest scan per wave 47 -> 28 events at the median) and
 // the two parts run at once. Part 1 (the slot's own wave) takes the openings T <= T_a; part 2 (a helper wave)
 // starts from an optimal capped allocation at T_a (the greedy's) and takes the openings above it,
@@ -1037,6 +1037,7 @@ struct ScanSplit {
 #ifdef HALDA_STAMPS
     unsigned long long *prof = nullptr;  // g_halda_scanprof of this wave (part 1 only)
 #endif
+    int cut8 = 4;  // the cut's rank, in eighths of the way up (both parts use the same)
 };
 
 // Rank of v among the 16 lanes of its DPP row (ties: the lower lane first).
@@ -1106,9 +1107,10 @@ __device__ bool kc_scan_incremental(const WaveCtx &w, const Inst &I, const SG &s
             const int n = sg.sum_i(has ? 1 : 0);
             const int r2 = rank16(v2, lane, std::make_integer_sequence<int, 15>{});
             // the cut (> T0; +inf: no opening at all)
-            // (rank 5/8 of the way up: part 1 leaves its leaf checks and phase 0 to other waves, so
-            // it takes the larger share of the range; measured against 4/8 and 6/8)
-            const double ta = sg.min_f64(has && r2 == (n - 1) * 5 / 8 ? v2 : kInf);
+            // (rank sp.cut8 / 8 of the way up, 4/8 by default: measured 3/8 .. 6/8 with five k-slot
+            // workgroups per CU; 5/8 was best at four, when part 1 first left its leaf checks and phase 0
+            // to other waves)
+            const double ta = sg.min_f64(has && r2 == (n - 1) * sp.cut8 / 8 ? v2 : kInf);
             t_stop = part == 1 ? ta : kInf;
             if (part > 1) {
                 T = ta;
@@ -1472,7 +1474,7 @@ __device__ int dp_pass_lanes(const WaveCtx &w, const Inst &I, const SG &sg, int6
 #ifdef HALDA_STAMPS
                                                                      , sp.prof
 #endif
-                                                                     });
+                                                                     , sp.cut8});
         wave_sync();
         return done(1);
     }

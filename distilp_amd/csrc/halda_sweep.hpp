@@ -1337,6 +1337,7 @@ struct SlotArgs {
     int check_wave;            // the wave that checks the split slot's leaves after its own slot (-1: none)
     int opt;                   // 1: an optimistic part 1 where its rows allow (0: the sequential order, a test path)
     int crit_w4;               // table share of the critical slot's wave, in quarters of the others'
+    int cut8;                  // the split scan's cut: rank cut8 / 8 of the way up (ScanSplit::cut8)
 };
 static_assert(kSegLanes == 16, "SplitArea holds 16 lanes per segment");
 
@@ -1754,8 +1755,9 @@ __device__ void kslot_helper(const SweepArgs &A, const SlotArgs &SA, const Kslot
                 WaveCtx w = kslot_ctx(A, SA, p, smem, seg);
                 w.st0 = ar->alt_e[h];  // this part's result, not the slot's st0
                 int64_t nodes = 0;
-                (void)kc_scan_incremental(w, I, sg, ar->s_inf, ar->best0, nodes, li,
-                                          ScanSplit{part, SA.n_parts, ar});
+                ScanSplit sp{part, SA.n_parts, ar};
+                sp.cut8 = SA.cut8;
+                (void)kc_scan_incremental(w, I, sg, ar->s_inf, ar->best0, nodes, li, sp);
             }
             pending = false;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1853,13 +1855,14 @@ __device__ void kslot_group(const SweepArgs &A, const SlotArgs &SA, const SweepB
         int wl = 0, nl = 0;
         SlotPick mine = {kInf, HALDA_STATUS_INFEASIBLE, 0};
 #ifdef HALDA_STAMPS
-        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0,
-                           int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
-                               ? g_halda_scanprof + (int64_t(blockIdx.x) * SA.n_slot + q) * kScanProf
-                               : nullptr};
+        ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0,
+                     int64_t(blockIdx.x) * SA.n_slot + q < kStampInst
+                         ? g_halda_scanprof + (int64_t(blockIdx.x) * SA.n_slot + q) * kScanProf
+                         : nullptr};
 #else
-        const ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0};
+        ScanSplit sp{q == SA.helper ? 1 : 0, SA.n_parts, split, false, SA.opt != 0};
 #endif
+        sp.cut8 = SA.cut8;
         if (f < nf)
             sweep_kslot(A, B, fd, int(f), SA.j[q], SA.r1[q], SA.tab[q], w, sg, mine, t_rec, sp, wl, nl);
         if (q == SA.helper && f < nf && sg.sl == 0 && split->pub == 0) split->pub = 2;  // did not scan: helpers skip
