@@ -17,6 +17,7 @@
 #define PY_SSIZE_T_CLEAN
 #define _GNU_SOURCE
 #include <Python.h>
+#include <structmember.h>
 #include <math.h>
 #include <pthread.h>
 #include <sched.h>
@@ -236,10 +237,18 @@ static int fast_dev(const Job *J, PyObject *d, Py_ssize_t g) {
 }
 
 /* Software prefetch ahead of the read-only pass: the profiles of a large batch are scattered Python
- * objects (the instance, its field dict, ~20 value objects and the nested FLOPs tables), so the pass
- * is bound by memory latency. Two stages: PF_FAR devices ahead the instance and its dict object,
- * PF_NEAR devices ahead the dict's entries and every value object they point at. Reads only. */
-enum { PF_FAR = 8, PF_NEAR = 3 };
+ * objects (the instance, its field dict and the dict's keys object, ~20 value objects, the nested FLOPs
+ * tables {Q: {"b_1": v}}), a chain of dependent cache misses per device, so the pass is bound by memory
+ * latency. A pipeline of prefetch stages runs ahead of the device being packed, each stage reading only
+ * what an earlier stage already brought in and prefetching the next level: PF_OBJ devices ahead the
+ * instance, PF_DICT its dict object, PF_KEYS the dict's keys object (the entries), PF_VALS every value
+ * object, PF_NEST the nested tables' keys objects, PF_ROW their row dicts. Reads only. */
+enum { PF_OBJ = 20, PF_DICT = 15, PF_KEYS = 10, PF_VALS = 6, PF_NEST = 3, PF_ROW = 1 };
+
+static void prefetch_lines(const void *p, int n) {
+    const char *c = (const char *)p;
+    for (int i = 0; i < n; ++i) __builtin_prefetch(c + 64 * i);
+}
 
 static void prefetch_values(PyObject *d) {
     Py_ssize_t pos = 0;
@@ -247,20 +256,48 @@ static void prefetch_values(PyObject *d) {
     while (PyDict_Next(d, &pos, &k, &v)) __builtin_prefetch(v);
 }
 
+/* the nested FLOPs tables of one device dict (values already cached): `keys` prefetches each table's keys
+ * object, else (keys cached) its Q row dict and that row's keys object */
+static void prefetch_tables(const Job *J, PyObject *d, int keys) {
+    PyObject *const t[3] = {FGET(d, scpu), FGET(d, sgpu_metal), FGET(d, sgpu_cuda)};
+    for (int a = 0; a < 3; ++a) {
+        if (!t[a] || !PyDict_CheckExact(t[a])) continue;
+        if (keys) {
+            prefetch_lines(((PyDictObject *)t[a])->ma_keys, 3);
+        } else {
+            PyObject *row = _PyDict_GetItem_KnownHash(t[a], J->Q, J->hQ);
+            if (row && PyDict_CheckExact(row)) prefetch_lines(((PyDictObject *)row)->ma_keys, 3);
+        }
+    }
+}
+
 static void *worker(void *arg) {
     const Job *J = (const Job *)arg;
     for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g) {
-        if (g + PF_FAR < J->hi) {
-            PyObject *o = J->devs[g + PF_FAR];
-            __builtin_prefetch(o);
-#if !DICTS_ON_CALLER
-            PyObject **dp = _PyObject_GetDictPtr(o);
-            if (dp) __builtin_prefetch(dp);
+        if (g + PF_OBJ < J->hi) __builtin_prefetch(J->devs[g + PF_OBJ]);
+        if (g + PF_DICT < J->hi) {
+#if DICTS_ON_CALLER
+            __builtin_prefetch(J->devs[g + PF_DICT]);
+#else
+            PyObject **dp = _PyObject_GetDictPtr(J->devs[g + PF_DICT]);
+            if (dp && *dp) __builtin_prefetch(*dp);
 #endif
         }
-        if (g + PF_NEAR < J->hi) {
-            PyObject *d = dev_dict(J->devs[g + PF_NEAR]);
+        if (g + PF_KEYS < J->hi) {
+            PyObject *d = dev_dict(J->devs[g + PF_KEYS]);
+            if (d) prefetch_lines(((PyDictObject *)d)->ma_keys, 12);
+        }
+        if (g + PF_VALS < J->hi) {
+            PyObject *d = dev_dict(J->devs[g + PF_VALS]);
             if (d) prefetch_values(d);
+        }
+        if (g + PF_NEST < J->hi) {
+            PyObject *d = dev_dict(J->devs[g + PF_NEST]);
+            if (d && fdict(d)) prefetch_tables(J, d, 1);
+        }
+        if (g + PF_ROW < J->hi) {
+            PyObject *d = dev_dict(J->devs[g + PF_ROW]);
+            if (d && fdict(d)) prefetch_tables(J, d, 0);
         }
         PyObject *d = dev_dict(J->devs[g]);
         if (!d || !fdict(d) || fast_dev(J, d, g)) *J->bail = 1;
@@ -529,7 +566,56 @@ done:
  * (halda_p_solver.py:356-357, dense_common.py:211-230): out[0][f] = sum t_comm and out[1][f] = sum xi
  * over the devices from the first (Python's `s = 0; for d in devs: s += ...`), out[2][f] = kappa: the
  * head's four terms, then the M1 devices' and then the M3 devices' RAM-headroom terms in index order.
- * IEEE double arithmetic in that order (built with -ffp-contract=off): the bits of the Python loops. */
+ * IEEE double arithmetic in that order (built with -ffp-contract=off): the bits of the Python loops.
+ * Fleets are independent: large tables are split over the packer's threads (each fleet's sums stay one
+ * scalar loop, so the bits do not depend on the split). */
+typedef struct {
+    const double *f64, *b64;
+    const int64_t *off, *heads;
+    const uint8_t *cls;
+    Py_ssize_t nd, nf, lo, hi;
+    int fout;
+    double f_out_b1, b_in, b_out, V;
+    double *out;
+    int bad;
+} ConstJob;
+
+static void *consts_range(void *arg) {
+    ConstJob *J = (ConstJob *)arg;
+    const Py_ssize_t nd = J->nd, nf = J->nf;
+    const double *f64 = J->f64, *b64 = J->b64;
+    const uint8_t *cls = J->cls, *flg = cls + nd;
+    const double *scpu = f64, *Tc = f64 + 2 * nd, *r2v = f64 + 6 * nd, *v2r = f64 + 7 * nd, *tcomm = f64 + 8 * nd,
+                 *sd = f64 + 9 * nd;
+    const double *ram = b64, *ccpu = b64 + nd, *swap = b64 + 5 * nd;
+    double *out = J->out;
+    for (Py_ssize_t f = J->lo; f < J->hi; ++f) {
+        const int64_t a = J->off[f], b = J->off[f + 1], h = J->heads[f];
+        if (a < 0 || b > nd || a > b || h < a || h >= b) {
+            J->bad = 1;
+            return NULL;
+        }
+        double t = 0.0, x = 0.0;
+        for (int64_t j = a; j < b; ++j) t += tcomm[j];
+        for (int64_t j = a; j < b; ++j) x += (r2v[j] + v2r[j]) * ((flg[j] & UMA) ? 0.0 : 1.0);
+        double total = 0.0;
+        if (J->fout && (flg[h] & CPU_RATE)) total = scpu[h] > 0.0 ? 0.0 + J->f_out_b1 / scpu[h] : 0.0;
+        total += (J->b_in / J->V + J->b_out) / Tc[h];
+        total += J->b_in / (J->V * sd[h]);
+        total += J->b_out / sd[h];
+        double tail = 0.0;
+        for (int pass = 1; pass <= 3; pass += 2)
+            for (int64_t j = a; j < b; ++j)
+                if (cls[j] == pass) tail += ((ccpu[j] - ram[j]) - swap[j]) / sd[j];
+        out[f] = t;
+        out[nf + f] = x;
+        out[2 * nf + f] = total + tail;
+    }
+    return NULL;
+}
+
+static int pack_threads(Py_ssize_t nd);
+
 static PyObject *consts(PyObject *self, PyObject *args) {
     (void)self;
     Py_buffer bf, bi, bu, bo, bh, bout;
@@ -545,35 +631,30 @@ static PyObject *consts(PyObject *self, PyObject *args) {
         goto done;
     }
     {
-        const double *f64 = (const double *)bf.buf;
-        const double *b64 = (const double *)bi.buf;
-        const int64_t *off = (const int64_t *)bo.buf, *heads = (const int64_t *)bh.buf;
-        const uint8_t *cls = (const uint8_t *)bu.buf, *flg = cls + nd;
-        const double *scpu = f64, *Tc = f64 + 2 * nd, *r2v = f64 + 6 * nd, *v2r = f64 + 7 * nd, *tcomm = f64 + 8 * nd,
-                     *sd = f64 + 9 * nd;
-        const double *ram = b64, *ccpu = b64 + nd, *swap = b64 + 5 * nd;
-        double *out = (double *)bout.buf;
-        for (Py_ssize_t f = 0; f < nf; ++f) {
-            const int64_t a = off[f], b = off[f + 1], h = heads[f];
-            if (a < 0 || b > nd || a > b || h < a || h >= b) {
-                PyErr_SetString(PyExc_ValueError, "consts: bad offsets");
-                goto done;
-            }
-            double t = 0.0, x = 0.0;
-            for (int64_t j = a; j < b; ++j) t += tcomm[j];
-            for (int64_t j = a; j < b; ++j) x += (r2v[j] + v2r[j]) * ((flg[j] & UMA) ? 0.0 : 1.0);
-            double total = 0.0;
-            if (fout && (flg[h] & CPU_RATE)) total = scpu[h] > 0.0 ? 0.0 + f_out_b1 / scpu[h] : 0.0;
-            total += (b_in / V + b_out) / Tc[h];
-            total += b_in / (V * sd[h]);
-            total += b_out / sd[h];
-            double tail = 0.0;
-            for (int pass = 1; pass <= 3; pass += 2)
-                for (int64_t j = a; j < b; ++j)
-                    if (cls[j] == pass) tail += ((ccpu[j] - ram[j]) - swap[j]) / sd[j];
-            out[f] = t;
-            out[nf + f] = x;
-            out[2 * nf + f] = total + tail;
+        int nt = pack_threads(nd);
+        if (nt < 1) nt = 1;
+        if (nt > 64) nt = 64;
+        if (nt > nf) nt = (int)(nf > 0 ? nf : 1);
+        ConstJob jobs[64];
+        pthread_t th[64];
+        int started = 0, bad = 0;
+        for (int t = 0; t < nt; ++t)
+            jobs[t] = (ConstJob){(const double *)bf.buf, (const double *)bi.buf, (const int64_t *)bo.buf,
+                                 (const int64_t *)bh.buf, (const uint8_t *)bu.buf, nd, nf, nf * t / nt,
+                                 nf * (t + 1) / nt, fout, f_out_b1, b_in, b_out, V, (double *)bout.buf, 0};
+        Py_BEGIN_ALLOW_THREADS /* plain arrays only, held by the buffers above */
+        for (int t = 1; t < nt; ++t) {
+            if (pthread_create(&th[t], NULL, consts_range, &jobs[t]) != 0) break;
+            started = t;
+        }
+        consts_range(&jobs[0]);
+        for (int t = started + 1; t < nt; ++t) consts_range(&jobs[t]); /* threads that did not start */
+        for (int t = 1; t <= started; ++t) pthread_join(th[t], NULL);
+        Py_END_ALLOW_THREADS
+        for (int t = 0; t < nt; ++t) bad |= jobs[t].bad;
+        if (bad) {
+            PyErr_SetString(PyExc_ValueError, "consts: bad offsets");
+            goto done;
         }
     }
     Py_INCREF(Py_None);
@@ -595,7 +676,7 @@ done:
  * obj[f], sets = the device indices of class 1 / 2 / 3 in device order (assign_sets,
  * dense_common.py:149-167). Each object is what cls.model_construct(w=..., n=..., k=..., obj_value=...,
  * sets=...) gives: the field dict, its own fields-set, no extra / private state. */
-static PyObject *s_dict, *s_fset, *s_extra, *s_priv, *s_w, *s_n, *s_k, *s_obj, *s_sets, *s_m[3];
+static PyObject *s_dict, *s_fset, *s_extra, *s_priv, *s_w, *s_n, *s_k, *s_obj, *s_sets, *s_m[3], *s_fields_tpl;
 
 static PyObject *int_list(const double *v, Py_ssize_t M) {
     PyObject *l = PyList_New(M);
@@ -609,6 +690,49 @@ static PyObject *int_list(const double *v, Py_ssize_t M) {
         PyList_SET_ITEM(l, i, o);
     }
     return l;
+}
+
+/* Where model_construct's four stores land in an instance of `cls`: the instance dict's offset and the
+ * byte offsets of the three BaseModel slots (member descriptors of object type). Resolved once per class
+ * from the type itself; when the class does not have that shape (another pydantic version, a subclass
+ * with a custom __setattr__ path for these names) `direct` stays 0 and the generic setattr is used. */
+typedef struct {
+    PyTypeObject *cls;
+    int direct;
+    Py_ssize_t fset, extra, priv;
+} Slots;
+static Slots g_slots;
+
+static Py_ssize_t member_offset(PyTypeObject *cls, PyObject *name) {
+    PyObject *d = _PyType_Lookup(cls, name); /* borrowed */
+    if (!d || !Py_IS_TYPE(d, &PyMemberDescr_Type)) return -1;
+    PyMemberDef *m = ((PyMemberDescrObject *)d)->d_member;
+    if ((m->type != T_OBJECT_EX && m->type != T_OBJECT) || (m->flags & READONLY)) return -1;
+    return m->offset;
+}
+
+static void resolve_slots(PyTypeObject *cls) {
+    if (g_slots.cls == cls) return;
+    Py_INCREF(cls); /* held: the cached offsets stay keyed to a live type */
+    Py_XDECREF(g_slots.cls);
+    g_slots.cls = cls;
+    g_slots.direct = 0;
+    g_slots.fset = member_offset(cls, s_fset);
+    g_slots.extra = member_offset(cls, s_extra);
+    g_slots.priv = member_offset(cls, s_priv);
+    /* model_construct stores through object.__setattr__ (the generic setattr): for a name the type
+     * resolves to an object-typed member descriptor that is a store at the member's offset, and for
+     * "__dict__" the instance dict slot */
+    g_slots.direct = g_slots.fset > 0 && g_slots.extra > 0 && g_slots.priv > 0 && cls->tp_dictoffset > 0;
+}
+
+static int put_slot(PyObject *o, Py_ssize_t off, PyObject *v) {
+    PyObject **p = (PyObject **)((char *)o + off);
+    PyObject *old = *p;
+    Py_INCREF(v);
+    *p = v;
+    Py_XDECREF(old);
+    return 0;
 }
 
 static PyObject *one_result(PyTypeObject *cls, PyObject *noargs, const double *xr, Py_ssize_t M, long long k, double obj,
@@ -639,15 +763,20 @@ static PyObject *one_result(PyTypeObject *cls, PyObject *noargs, const double *x
     }
     if (PyDict_SetItem(d, s_sets, sets)) goto fail;
     Py_CLEAR(sets);
-    if (!(fs = PySet_New(NULL))) goto fail;
-    PyObject *names[5] = {s_w, s_n, s_k, s_obj, s_sets};
-    for (int a = 0; a < 5; ++a)
-        if (PySet_Add(fs, names[a])) goto fail;
+    if (!(fs = PySet_New(s_fields_tpl))) goto fail; /* {w, n, k, obj_value, sets}: a copy, no re-hashing */
     /* object.__new__(cls) and object.__setattr__ of the four slots, as model_construct does */
     if (!(o = PyBaseObject_Type.tp_new(cls, noargs, NULL))) goto fail;
-    if (PyObject_GenericSetAttr(o, s_dict, d) || PyObject_GenericSetAttr(o, s_fset, fs) ||
-        PyObject_GenericSetAttr(o, s_extra, Py_None) || PyObject_GenericSetAttr(o, s_priv, Py_None))
+    if (g_slots.cls == cls && g_slots.direct) {
+        PyObject **dp = _PyObject_GetDictPtr(o);
+        if (!dp) goto fail;
+        put_slot(o, (char *)dp - (char *)o, d);
+        put_slot(o, g_slots.fset, fs);
+        put_slot(o, g_slots.extra, Py_None);
+        put_slot(o, g_slots.priv, Py_None);
+    } else if (PyObject_GenericSetAttr(o, s_dict, d) || PyObject_GenericSetAttr(o, s_fset, fs) ||
+               PyObject_GenericSetAttr(o, s_extra, Py_None) || PyObject_GenericSetAttr(o, s_priv, Py_None)) {
         goto fail;
+    }
     Py_DECREF(d);
     Py_DECREF(fs);
     return o;
@@ -708,6 +837,7 @@ static PyObject *results(PyObject *self, PyObject *args) {
      * collections that walk every object the caller holds (a batch's 262,144 DeviceProfile objects and
      * their dicts: one full collection costs more than building all 4,096 results) */
     gc_was = PyGC_Disable();
+    resolve_slots((PyTypeObject *)cls);
     if (!(noargs = PyTuple_New(0)) || !(ret = PyList_New(nf))) goto done;
     const double *x = (const double *)bx.buf, *obj = (const double *)bo.buf;
     const int64_t *row = (const int64_t *)br.buf, *kk = (const int64_t *)bk.buf, *off = (const int64_t *)boff.buf;
@@ -757,5 +887,12 @@ PyMODINIT_FUNC PyInit__fleetpack(void) {
     STR(s_priv, "__pydantic_private__") STR(s_w, "w") STR(s_n, "n") STR(s_k, "k") STR(s_obj, "obj_value")
     STR(s_sets, "sets") STR(s_m[0], "M1") STR(s_m[1], "M2") STR(s_m[2], "M3")
 #undef STR
+    {
+        PyObject *names = PyTuple_Pack(5, s_w, s_n, s_k, s_obj, s_sets);
+        if (!names) return NULL;
+        s_fields_tpl = PyFrozenSet_New(names);
+        Py_DECREF(names);
+        if (!s_fields_tpl) return NULL;
+    }
     return PyModule_Create(&mod);
 }

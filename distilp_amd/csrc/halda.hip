@@ -33,6 +33,20 @@
 #include "halda.h"
 
 namespace {
+// Page-locked host blocks handed out by halda_host_alloc: a call whose every host array lies in one of
+// them copies straight between them and device memory (no staging memcpy through the context's buffer).
+std::mutex g_host_mu;
+std::vector<std::pair<uintptr_t, size_t>> g_host_blocks;
+
+bool in_host_block(const void *p, size_t bytes) {
+    if (!p) return true;  // an absent optional array
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lock(g_host_mu);
+    for (const auto &b : g_host_blocks)
+        if (a >= b.first && a - b.first <= b.second && bytes <= b.second - (a - b.first)) return true;
+    return false;
+}
+
 
 #include "halda_prims.hpp"
 #include "halda_solve.hpp"
@@ -112,6 +126,7 @@ struct Ctx {
     bool k1_force_dp = false;      // fused sweep, test path: every register-launch k = 1 solve by k1_dp
     bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
     bool host_copy = false;        // halda_solve_fleets_host: PCIe copies even for small calls (HALDA_HOST_PATH=copy)
+    bool fused_screen = true;      // a settled batch screens inside its k = 1 kernel (HALDA_FUSED_SCREEN=0: screen launch)
     bool last_fleet_fused = false;
     int path_gen = 0;              // bumped by halda_set_fleets_path: prepared plans re-plan on their next launch
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
@@ -348,7 +363,17 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     const int launch_id = ++ctx->launch_id;  // tags this launch's flags: k = 1 hand-backs, k > 1 work (no reset)
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     const int64_t lds1 = make_k1_slice(std::min(mmax, kK1MaxM)).total;
-    {
+    if (settled && ctx->fused_screen) {
+        // a settled batch: no screen launch -- the persistent k = 1 kernel writes the settled instances'
+        // outputs and screens every other instance on its way (halda_solve_k1_settled_kernel)
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
+        int per_cu = 0;
+        HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_settled_kernel), lds1, &per_cu));
+        const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
+        hipLaunchKernelGGL(halda_solve_k1_settled_kernel, dim3(grid), dim3(64), size_t(lds1), stream, in, out, cls,
+                           mmax, hb_flag, launch_id, settled, gen_flag, in.max_R1, int(tab), int(tab_kc));
+        HIP_TRY(hipGetLastError());
+    } else {
         // screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
@@ -1083,6 +1108,8 @@ int halda_init(int device_ordinal, void **ctx_out) {
     c->host_copy = hp && std::strcmp(hp, "copy") == 0;
     const char *rs = std::getenv("HALDA_RESIDENT");
     c->resident = !(rs && std::strcmp(rs, "0") == 0);
+    const char *fs = std::getenv("HALDA_FUSED_SCREEN");  // A/B: the screen launch before a settled batch's k = 1 kernel
+    c->fused_screen = !(fs && std::strcmp(fs, "0") == 0);
     const char *kw = std::getenv("HALDA_KSLOT_CRIT_W4");  // diagnostic A/B of the critical slot's table share
     if (kw && std::atoi(kw) > 0) c->kslot_crit_w4 = std::atoi(kw);
     const char *kc8 = std::getenv("HALDA_KSLOT_CUT8");  // diagnostic A/B of the split scan's cut
@@ -1111,6 +1138,28 @@ int halda_resident_release(void *ctx) {
     if (!resident_stop(c, std::chrono::milliseconds(5000)))
         return fail(HALDA_E_HIP, "resident solver: the wave did not leave within 5 s");
     return HALDA_OK;
+}
+
+int halda_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr || bytes == 0) return fail(HALDA_E_ARG, "halda_host_alloc: NULL ptr or zero bytes");
+    *ptr = nullptr;
+    HIP_TRY(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lock(g_host_mu);
+    g_host_blocks.emplace_back(reinterpret_cast<uintptr_t>(*ptr), bytes);
+    return HALDA_OK;
+}
+
+void halda_host_free(void *ptr) {
+    if (!ptr) return;
+    {
+        std::lock_guard<std::mutex> lock(g_host_mu);
+        for (size_t i = 0; i < g_host_blocks.size(); ++i)
+            if (g_host_blocks[i].first == reinterpret_cast<uintptr_t>(ptr)) {
+                g_host_blocks.erase(g_host_blocks.begin() + i);
+                break;
+            }
+    }
+    (void)hipHostFree(ptr);
 }
 
 void halda_free(void *ctx) {
@@ -1713,6 +1762,7 @@ void halda_fleets_group_free(void *group) {
 // Synchronous halda_solve_fleets on HOST arrays: copies the table in, solves, copies results out.
 constexpr size_t kZeroCopyBytes = size_t(1) << 20;
 
+
 int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fleets *fh, const int32_t *ks,
                             int32_t n_k, halda_fleet_result *out_h) {
     Ctx *c = static_cast<Ctx *>(ctx);
@@ -1765,7 +1815,24 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
         c->pinned_bytes = off;
     }
     char *pin = static_cast<char *>(c->pinned);
+    const bool zc = off <= kZeroCopyBytes && !c->host_copy;
+    // every array in halda_host_alloc blocks (the batch API's workspaces): DMA straight from / to them
+    bool direct = !zc;
+    if (direct) {
+        const double *fa[16] = {fh->scpu_b1, fh->sgpu_b1, fh->T_cpu, fh->T_gpu, fh->t_kvcpy_cpu, fh->t_kvcpy_gpu,
+                                fh->t_ram2vram, fh->t_vram2ram, fh->t_comm, fh->s_disk, fh->d_avail_ram, fh->c_cpu,
+                                fh->c_gpu, fh->d_avail_cuda, fh->d_avail_metal, fh->swap};
+        for (int a = 0; a < 16 && direct; ++a) direct = fa[a] && in_host_block(fa[a], 8 * nd);
+        direct = direct && in_host_block(fh->dev_off, 8 * (nf + 1)) && fh->os_class && fh->flags &&
+                 in_host_block(fh->os_class, nd) && in_host_block(fh->flags, nd) &&
+                 in_host_block(out_h->x_off, xsel ? 8 * size_t(nf) * n_k : 0) &&
+                 in_host_block(out_h->best_k, 4 * nf) && in_host_block(out_h->obj_value, 8 * nf) &&
+                 in_host_block(out_h->w, 4 * nd) && in_host_block(out_h->n, 4 * nd) &&
+                 in_host_block(out_h->obj_by_k, 8 * nf * n_k) && in_host_block(out_h->status, 4 * nf * n_k) &&
+                 in_host_block(out_h->x, 8 * xs) && in_host_block(out_h->c, 8 * xs);
+    }
     auto up = [&](size_t o, const void *src, size_t bytes) {
+        if (direct) return hipMemcpyAsync(static_cast<char *>(c->scratch) + o, src, bytes, hipMemcpyHostToDevice, s);
         std::memcpy(pin + o, src, bytes);
         return hipSuccess;
     };
@@ -1788,11 +1855,10 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
     // table from and write the results to the pinned buffer itself, across PCIe, and the host polls
     // the completion event instead of sleeping in a stream synchronisation
     if (xsel) HIP_TRY(up(o_xoff, out_h->x_off, 8 * size_t(nf) * n_k));
-    const bool zc = off <= kZeroCopyBytes && !c->host_copy;
     if (zc) {
         if (!c->pinned_dev) HIP_TRY(hipHostGetDevicePointer(&c->pinned_dev, c->pinned, 0));
         base = static_cast<char *>(c->pinned_dev);
-    } else {
+    } else if (!direct) {
         HIP_TRY(hipMemcpyAsync(base, pin, o_bk, hipMemcpyHostToDevice, s));  // the table (and x_off)
     }
     auto F64 = [&](int a) { return reinterpret_cast<const double *>(base + o_f64 + 8 * nd * a); };
@@ -1845,6 +1911,20 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
         while ((q = hipEventQuery(c->ev_host)) == hipErrorNotReady) {
         }
         HIP_TRY(q);
+    } else if (direct) {
+        auto dn = [&](void *dst, size_t o, size_t bytes) {
+            return dst ? hipMemcpyAsync(dst, base + o, bytes, hipMemcpyDeviceToHost, s) : hipSuccess;
+        };
+        HIP_TRY(dn(out_h->best_k, o_bk, 4 * nf));
+        HIP_TRY(dn(out_h->obj_value, o_obj, 8 * nf));
+        HIP_TRY(dn(out_h->w, o_w, 4 * nd));
+        HIP_TRY(dn(out_h->n, o_n, 4 * nd));
+        HIP_TRY(dn(out_h->obj_by_k, o_obk, 8 * nf * n_k));
+        HIP_TRY(dn(out_h->status, o_st, 4 * nf * n_k));
+        HIP_TRY(dn(out_h->x, o_x, 8 * xs));
+        HIP_TRY(dn(out_h->c, o_c, 8 * xs));
+        HIP_TRY(hipStreamSynchronize(s));
+        return HALDA_OK;
     } else {
         HIP_TRY(hipMemcpyAsync(pin + o_bk, base + o_bk, off - o_bk, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

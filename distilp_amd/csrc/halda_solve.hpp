@@ -61,12 +61,13 @@ struct ScreenOut {
 
 __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i0, int lane,
                                     int mmax, int r1max, int tab, int tab_kc, ScreenOut &so,
-                                    const uint8_t *settled, int *gen_flag, int launch_id) {
+                                    const uint8_t *settled, int *gen_flag, int launch_id, int nlim = kScreenPer) {
     // lane g < kScreenPer: header of instance i0 + g. Loads are branch-free (lanes
     // without an instance read a valid element and discard it) so that each round
-    // trip's loads issue before the first wait.
+    // trip's loads issue before the first wait. nlim < kScreenPer: only instances i0 .. i0 + nlim - 1
+    // (the settled k = 1 kernel's screen of one instance, halda_solve_k1_settled_kernel).
     const int64_t my = i0 + lane;
-    const bool own = lane < kScreenPer && my < B.n_inst;
+    const bool own = lane < nlim && lane < kScreenPer && my < B.n_inst;
     const int64_t mc = own ? my : i0;
     const int N0 = B.n_cols[mc], m0 = B.n_rows[mc];
     const int64_t co0 = B.col_off[mc], ro0 = B.row_off[mc], cs0 = B.csr_off[mc];
@@ -121,6 +122,7 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     int e_prev = -1, m_prev = -1;
 #pragma unroll
     for (int g = 0; g < kScreenPer; ++g) {
+        if (g >= nlim) break;
         const int stg = __shfl(status, g), eg = __shfl(eqs0, g);
         const int Mg = __shfl(M, g);
         const int64_t cg = shfl64(co0, g);
@@ -150,7 +152,7 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
     int verdict = CLS_DONE, vstatus = status;  // lane g: outcome of instance g
 #pragma unroll
     for (int g = 0; g < kScreenPer; ++g) {
-        if (i0 + g >= B.n_inst) break;
+        if (i0 + g >= B.n_inst || g >= nlim) break;
         const int stg = __shfl(status, g);
         if (stg) continue;
         const int Mg = __shfl(M, g), eg = __shfl(eqs, g), pre = pre_[g];
@@ -217,6 +219,15 @@ __device__ inline void screen_group(const halda_batch &B, const halda_result &Rz
             }
         }
     }
+}
+
+// The screen of ONE instance by one wave (the settled k = 1 kernel's slow path: shapes its fast path does not
+// take); returns the verdict on every lane.
+__device__ inline int screen_one(const halda_batch &B, const halda_result &Rz, uint8_t *cls, int64_t i, int lane,
+                                       int mmax, int r1max, int tab, int tab_kc, int *gen_flag, int launch_id) {
+    ScreenOut so;
+    screen_group(B, Rz, cls, i, lane, mmax, r1max, tab, tab_kc, so, nullptr, gen_flag, launch_id, 1);
+    return __shfl(so.verdict, 0);
 }
 
 // ---------------------------------------------------------------- solve
@@ -2205,8 +2216,27 @@ constexpr int kRpSlots = 5;  // row pointers rp[0 .. ncap] per lane: ncap <= 64 
 // device i's objective entries (shuffled from lane i) and land in lane i's
 // registers. Fills d. Returns 0 ok, 1 not a HALDA MILP, 2 not in this shape
 // (the caller then runs the generic decode).
+//
+// kScreen (halda_solve_k1_settled_kernel: no screen launch before it): the screen's verdict on this
+// instance rides the same round trips -- the equality row's extent and bounds with round trip 1, its
+// entries with round trip 2 (the w lower bounds are round trip 1's) -- and is decided right after round
+// trip 2 by the screen's own rules and precedence (screen_group: a non-HALDA equality row, then bound
+// infeasibility, then a table beyond the launches' slices, then c[C] > 0 for the k > 1 launch). An
+// instance the screen would not class CLS_K1 gets the screen's outputs (status / cls / the k > 1 flag)
+// and 3 is returned; sc->screened says whether that point was reached (a return 2 before it leaves the
+// screen to the caller).
+struct K1Screen {
+    int mmax, r1max, tab, tab_kc;
+    int *gen_flag;
+    int launch_id;
+    uint8_t *cls;
+    const halda_result *Rz;
+    bool screened;
+};
+
+template <bool kScreen = false>
 __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *scol_raw, unsigned char *sval_raw,
-                         Inst &I, int lane, Dev &d, int &sumlo) {
+                         Inst &I, int lane, Dev &d, int &sumlo, K1Screen *sc = nullptr) {
     const int M = I.M, ncyc = 2 * M, ncap = I.m - 1 - ncyc;
     // M >= 4: the staged 16-B chunks past a segment's end stay inside the equality row
     if (M < 4 || ncap < 0 || ncap > 64 * kCapSlots || ncyc > 64 * kCycSlots) return 2;
@@ -2243,6 +2273,13 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
     I.Wd = B.row_ub[I.ro + I.m - 1];
     I.kc = B.c[co + I.iC];
     I.W = int(I.Wd);
+    int eqs = 0, eqe = 0;
+    double Wl = 0.0;
+    if constexpr (kScreen) {  // the equality row's extent and lower bound (screen_group's round trip 2)
+        eqs = I.rp[I.m - 1];
+        eqe = I.rp[I.m];
+        Wl = B.row_lb[I.ro + I.m - 1];
+    }
     int dbad = iz != 0 || cz != 0.0 || lz != 0.0 || uz != kInf || lbv[1] < 0.0;
 #pragma unroll
     for (int b = 0; b < 6; ++b) dbad |= ig[b] != 1;
@@ -2301,6 +2338,40 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
     }
     stage_wait();  // staged entries and zeroed counters visible
     HALDA_DSTAMP(2);
+    // the screen's verdict needs the equality row's entries, loaded with the first cycle half below
+    // (screen_group's round trip 3): by then the capacity rows' registers are free
+    const bool eq_ext = eqe - eqs == M;
+    bool lb_inf = false;
+    if constexpr (kScreen) lb_inf = wave_or(act && (int(ceil(lbv[0])) > I.W || lbv[0] < 0.0)) != 0;
+    auto screen_verdict = [&](int ecol, double eval) -> bool {
+        // screen_group's verdict, in its precedence (everything it reads is in): UNSUPPORTED (equality
+        // row), INFEASIBLE (w lower bounds), TOO_LARGE (the launches' slices), else CLS_GEN for c[C] > 0
+        sc->screened = true;
+        int st = 0, v = CLS_K1;
+        const bool rowbad = !(Wl == I.Wd) || !(I.Wd >= 0.0 && I.Wd < 1e6 && I.Wd == floor(I.Wd)) || !eq_ext;
+        if (rowbad || wave_or(act && (ecol != lane || eval != 1.0))) {
+            st = HALDA_STATUS_UNSUPPORTED;
+        } else {
+            if (lb_inf || sumlo > I.W) {
+                st = HALDA_STATUS_INFEASIBLE;
+            } else {
+                const int R1 = I.W - sumlo + 1;
+                const bool kc = I.kc > 0.0;
+                if (R1 > sc->r1max || int64_t(M) * odd_stride(R1) > (kc ? sc->tab_kc : sc->tab)) st = HALDA_STATUS_TOO_LARGE;
+                else if (kc) v = CLS_GEN;
+            }
+        }
+        if (st || v != CLS_K1) {
+            if (lane == 0) {
+                sc->cls[I.inst] = uint8_t(st ? CLS_DONE : v);
+                if (st) write_done(*sc->Rz, I.inst, st, 0);
+                if (v == CLS_GEN) *sc->gen_flag = sc->launch_id;  // the k > 1 launch of this batch has work
+            }
+            return true;
+        }
+        if (lane == 0) sc->cls[I.inst] = CLS_K1;  // (a hand-back below rewrites it)
+        return false;
+    };
 #pragma unroll
     for (int j = 0; j < kCapSlots; ++j) {
         const int r = lane + 64 * j;
@@ -2336,6 +2407,15 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
         wave_sync();  // the previous segment's readers are done
         scol = reinterpret_cast<const int *>(scol_raw) + stage_lds(B.col_idx + hb[h], 4 * hn, scol_raw, lane) / 4;
         sval = reinterpret_cast<const double *>(sval_raw) + stage_lds(B.val + hb[h], 8 * hn, sval_raw, lane) / 8;
+        if constexpr (kScreen) {
+            if (h == 0) {
+                const int ei = eq_ext ? eqs + li : 0;
+                const int c0 = B.col_idx[ei];
+                const double v0 = B.val[ei];
+                stage_wait();
+                if (screen_verdict(act ? c0 : lane, act ? v0 : 1.0)) return 3;
+            }
+        }
         stage_wait();
         if (h == 0) HALDA_DSTAMP(4);
         else HALDA_DSTAMP(5);
@@ -2524,14 +2604,26 @@ __device__ inline void k1_finish(const halda_result &Rz, uint8_t *cls, const Ins
 
 // One k = 1 instance (lane = device) from decode to x; hands the instance to the
 // general kernel (cls = CLS_GEN) when the fast path does not apply.
+template <bool kScreen = false>
 __device__ void solve_k1(const halda_batch &B, const halda_result &Rz, uint8_t *cls, const WaveCtx &w,
                          unsigned char *scol, unsigned char *sval, Inst I, int lane, int *hb_flag,
-                         int launch_id) {
+                         int launch_id, K1Screen *sc = nullptr) {
     HALDA_STAMP(0);
     Dev d = {};
     int sumlo = 0;
-    const int fast = decode_k1(B, w, scol, sval, I, lane, d, sumlo);
+    const int fast = decode_k1<kScreen>(B, w, scol, sval, I, lane, d, sumlo, sc);
     HALDA_PSTAMP(1);
+    if (kScreen && fast == 3) {  // the screen's verdict is written (not a k = 1 fast-path instance)
+        wave_sync();
+        return;
+    }
+    if (kScreen && fast == 2 && !sc->screened) {
+        // this shape leaves decode_k1 before its screen point: the screen's own code on this one instance
+        wave_sync();
+        if (screen_one(B, Rz, cls, I.inst, lane, sc->mmax, sc->r1max, sc->tab, sc->tab_kc, sc->gen_flag, launch_id) !=
+            CLS_K1)
+            return;  // settled or classed for the general launches
+    }
     if (fast == 2) {  // another row order / shape: the general kernel (generic decode) takes it
         if (lane == 0) {
             cls[I.inst] = CLS_GEN1;
@@ -2598,6 +2690,70 @@ __global__ __launch_bounds__(256) void halda_screen_kernel(halda_batch B, halda_
     if (i0 >= B.n_inst) return;
     ScreenOut so;
     screen_group(B, Rz, cls, i0, lane, mmax, r1max, tab, tab_kc, so, settled, gen_flag, launch_id);
+}
+
+// The k = 1 kernel of a settled batch (halda_solve_batch_device_settled) with no screen launch before
+// it: the caller's settled instances get the screen's INFEASIBLE outputs lane-parallel (their rows are
+// never read), and every other instance is screened by its own wave on the way -- the screen's verdict
+// rides decode_k1's round trips (kScreen), so a k = 1 instance costs no round trip beyond the fast
+// path's own. What the screen would not class CLS_K1 is written as the screen writes it (status, or
+// cls + the k > 1 launch's flag) for the general launches behind this one.
+__global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_settled_kernel(
+    halda_batch B, halda_result Rz, uint8_t *cls, int mmax, int *hb_flag, int launch_id, const uint8_t *settled,
+    int *gen_flag, int r1max, int tab, int tab_kc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const K1Slice sl = make_k1_slice(min(mmax, kK1MaxM));
+    WaveCtx w = {};
+    w.rows = reinterpret_cast<int2 *>(smem + sl.rows);
+    w.cyc = reinterpret_cast<double *>(smem + sl.cyc);
+    w.cost = reinterpret_cast<double *>(smem + sl.cost);
+    w.cnt = reinterpret_cast<int *>(smem + sl.cnt);
+    unsigned char *scol = smem + sl.stage;
+    unsigned char *sval = smem + sl.stage + kStageColBytes;
+    K1Screen sc{mmax, r1max, tab, tab_kc, gen_flag, launch_id, cls, &Rz, false};
+    const int S = gridDim.x;
+    for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
+        const int64_t mine = base + int64_t(lane) * S;
+        const bool in = mine < B.n_inst;
+        const bool done = in && settled[in ? mine : 0] != 0;
+        if (done) {  // the screen's outputs for a settled instance (screen_group: hint)
+            cls[mine] = CLS_DONE;
+            write_done(Rz, int(mine), HALDA_STATUS_INFEASIBLE, 0);
+        }
+        uint64_t todo = __ballot(in && !done);
+        while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t i = base + int64_t(bit) * S;
+            const int N = B.n_cols[i], m = B.n_rows[i];
+            const int M = N >= 1 ? (N - 1) / 7 : 0;
+            sc.screened = false;
+            if (N < 1 || (N - 1) % 7 != 0 || m < 1 || M < 1 || M > min(mmax, kK1MaxM)) {
+                // not a k = 1 fast-path shape: the screen's own code decides (and writes) it
+                if (screen_one(B, Rz, cls, i, lane, mmax, r1max, tab, tab_kc, gen_flag, launch_id) == CLS_K1 &&
+                    lane == 0) {
+                    cls[i] = CLS_GEN1;  // (M > 64 is classed CLS_GEN1 by the screen itself)
+                    *hb_flag = launch_id;
+                }
+                wave_sync();
+                continue;
+            }
+            Inst I;
+            I.inst = int(i);
+            I.m = m;
+            I.M = M;
+            I.iC = 7 * M;
+            I.invM = 1.0f / float(M);
+            I.co = B.col_off[i];
+            I.ro = B.row_off[i];
+            I.rp = B.row_ptr + B.csr_off[i];
+            I.Wd = 0.0;
+            I.W = 0;
+            I.kc = 0.0;
+            solve_k1<true>(B, Rz, cls, w, scol, sval, I, lane, hb_flag, launch_id, &sc);
+        }
+    }
 }
 
 // k = 1 fast path: persistent 64-thread workgroups (one wave each) over the

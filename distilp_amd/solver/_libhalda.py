@@ -85,7 +85,7 @@ EXPORTS = ("halda_version", "halda_init", "halda_solve_batch", "halda_solve_batc
            "halda_solve_fleets_sharded", "halda_fleets_plan_create", "halda_fleets_plan_launch",
            "halda_fleets_plan_free", "halda_solve_fleets_sharded_emulated", "halda_fleets_plan_launch_many",
            "halda_fleets_group_create", "halda_fleets_group_launch", "halda_fleets_group_free",
-           "halda_resident_release")
+           "halda_resident_release", "halda_host_alloc", "halda_host_free")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -155,6 +155,10 @@ def load_library(path: Path | str | None = None):
         lib.halda_free.restype = None
         lib.halda_resident_release.argtypes = [ctypes.c_void_p]
         lib.halda_resident_release.restype = ctypes.c_int
+        lib.halda_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+        lib.halda_host_alloc.restype = ctypes.c_int
+        lib.halda_host_free.argtypes = [ctypes.c_void_p]
+        lib.halda_host_free.restype = None
         if path is None:
             _lib = lib
         return lib

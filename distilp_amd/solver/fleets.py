@@ -236,17 +236,66 @@ _PACKER = _load_packer()
 _TLS = threading.local()
 
 
-def _scratch(kind: str, shapes) -> tuple:
+class _HostBlock:
+    """One block of page-locked host memory from libhalda (halda_host_alloc), freed with its last view.
+    halda_solve_fleets_host DMAs straight from / to arrays that all lie in such blocks (include/halda.h)."""
+
+    def __init__(self, nbytes: int):
+        from ._libhalda import last_error, load_library
+
+        self.lib = load_library()
+        p = ctypes.c_void_p()
+        rc = self.lib.halda_host_alloc(nbytes, ctypes.byref(p))
+        if rc != 0:
+            raise RuntimeError(f"halda_host_alloc({nbytes}) failed ({rc}): {last_error(self.lib)}")
+        self.ptr = p.value
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                self.lib.halda_host_free(self.ptr)
+            except Exception:  # noqa: BLE001 -- interpreter teardown: the process's memory goes with it
+                pass
+            self.ptr = None
+
+
+_PINNED_OK = True  # False once page-locked memory could not be had (no GPU runtime): pageable workspaces
+
+
+def _host_arrays(shapes) -> tuple:
+    """Arrays of `shapes` ((shape, dtype) each, 256-B aligned) carved from one _HostBlock."""
+    offs, o = [], 0
+    for sh, dt in shapes:
+        offs.append(o)
+        o += (int(np.prod(sh)) * np.dtype(dt).itemsize + 255) & ~255
+    blk = _HostBlock(max(o, 256))
+    raw = (ctypes.c_char * max(o, 256)).from_address(blk.ptr)
+    raw._owner = blk  # the views keep the ctypes array alive, and it the block
+    return tuple(np.frombuffer(raw, dt, int(np.prod(sh)), off).reshape(sh) for (sh, dt), off in zip(shapes, offs))
+
+
+def _scratch(kind: str, shapes, pinned: bool = False) -> tuple:
     """The calling thread's reusable arrays for `kind` ((shape, dtype) each), kept between calls while the
     shapes repeat: a batch of 4,096 C3 fleets needs ~33 MB of table and ~30 MB of results, whose first
-    touch of fresh pages costs more than the pass that fills them. One set per kind and thread."""
+    touch of fresh pages costs more than the pass that fills them. One set per kind and thread. `pinned`:
+    in page-locked memory (_host_arrays), so that the GPU call copies them by DMA with no staging copy."""
     ws = getattr(_TLS, "scratch", None)
     if ws is None:
         ws = _TLS.scratch = {}
-    key = tuple((tuple(np.atleast_1d(sh).tolist()), np.dtype(dt).str) for sh, dt in shapes)
+    key = (pinned,) + tuple((tuple(np.atleast_1d(sh).tolist()), np.dtype(dt).str) for sh, dt in shapes)
     hit = ws.get(kind)
     if hit is None or hit[0] != key:
-        hit = ws[kind] = (key, tuple(np.empty(sh, dt) for sh, dt in shapes))
+        global _PINNED_OK
+        ws.pop(kind, None)  # the old set goes first (a pinned block is freed with its views)
+        arrs = None
+        if pinned and _PINNED_OK:
+            try:
+                arrs = _host_arrays(shapes)
+            except (RuntimeError, OSError, ImportError):  # no GPU runtime here: pageable workspaces
+                _PINNED_OK = False
+        if arrs is None:
+            arrs = tuple(np.empty(sh, dt) for sh, dt in shapes)
+        hit = ws[kind] = (key, arrs)
     return hit[1]
 
 
@@ -264,7 +313,7 @@ def fleet_table(fleets: Sequence[Sequence[DeviceProfile]], model: ModelProfile, 
     shapes = (((len(F64_FIELDS), nd), np.float64), ((len(BYTE_FIELDS), nd), np.float64), ((2, nd), np.uint8),
               (nf + 1, np.int64), (nf, np.int64))
     if _reuse:
-        f64, b64, u8, off, heads = _scratch("table", shapes)
+        f64, b64, u8, off, heads = _scratch("table", shapes, pinned=True)
     else:
         f64, b64, u8, off, heads = (np.empty(sh, dt) for sh, dt in shapes)
     _PACKER.pack(fleets, model.Q, "b_1" in model.f_q, "b_1" in model.f_out, f64, b64, u8, off, heads)
@@ -627,7 +676,12 @@ def solve_table(table: FleetTable, model: ModelProfile, ks: Sequence[int], kv_fa
         xs = 7 * int(fs.max_devices) + 1 if want_x else 0
         ext = nf * nk * xs
     if _reuse:
-        fbuf, ibuf = _scratch("solve", ((nf + nf * nk + 2 * ext, np.float64), (nf + 2 * nd + nf * nk, np.int32)))
+        fbuf, ibuf = _scratch("solve", ((nf + nf * nk + 2 * ext, np.float64), (nf + 2 * nd + nf * nk, np.int32)),
+                              pinned=True)
+        if xsel is not None:  # x_off in page-locked memory too: every array of the call is, so it DMAs directly
+            (xs_pin,) = _scratch("xoff", (((len(xsel),), np.int64),), pinned=True)
+            xs_pin[:] = xsel
+            xsel = xs_pin
     else:
         fbuf = np.zeros(nf + nf * nk + 2 * ext)
         ibuf = np.zeros(nf + 2 * nd + nf * nk, np.int32)

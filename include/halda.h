@@ -292,6 +292,14 @@ int halda_solve_fleets_host(void *ctx, const halda_model *model, const halda_fle
  * runs); the next one-fleet call relaunches it. For callers about to synchronise the whole device. */
 int halda_resident_release(void *ctx);
 
+/* Page-locked host memory for halda_solve_fleets_host's arrays. When EVERY array of the call's fleets and
+ * results (and x_off) lies in blocks from halda_host_alloc, a call above the zero-copy size copies straight
+ * between them and device memory (one DMA per array) instead of staging both ways through the context's
+ * own pinned buffer with host memcpys -- the batch API packs its fleet table into such a block
+ * (distilp_amd/solver/fleets.py). The results are the same either way. */
+int halda_host_alloc(size_t bytes, void **ptr);
+void halda_host_free(void *ptr);
+
 /* Several GPUs from one process: a context per device (ordinals may repeat), and
  * halda_solve_fleets_host over all of them -- the fleets are dealt out in contiguous blocks, one host
  * thread per device, results written at each block's offsets. Fleets are independent, so no

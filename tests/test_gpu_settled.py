@@ -72,3 +72,54 @@ def test_settled_batch_equals_synchronous_solve(llama_online_model, M, nf, ks, m
         assert np.array_equal(got["x"][a:b], want.x[a:b])
     if not opt.any():
         assert (got["x"] == -3.0).all()
+
+
+@pytest.mark.parametrize("flags", ["none", "proved"])
+def test_fused_screen_equals_screen_launch_on_hostile_batches(llama_online_model, flags):
+    """A settled batch is screened inside its k = 1 kernel (halda_solve_k1_settled_kernel: no screen launch).
+    Every instance the caller leaves unflagged gets the screen's own verdict there -- on fleets of 1 to 80
+    devices (the k = 1 fast path's shapes, the small ones it hands back, a wide fleet for the general
+    launch), k > 1 instances for the k > 1 launch, and corrupted instances: an equality-row coefficient 2,
+    swapped equality-row columns, row_lb != row_ub and a fractional W on the equality row, a negative and
+    a NaN w lower bound. Flags "none" screens every instance in the k = 1 kernel, "proved" the ones the
+    caller's own proof leaves. Status, obj_lin, dual_bound, gap, nodes and x equal the screen launch's."""
+    import torch
+
+    from distilp_amd.common import DeviceProfile
+
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ks = [1, 2, 4, 5]
+    sizes = [1, 2, 3, 5, 16, 64, 64, 64, 64, 64, 64, 16, 80]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(7100 + s, M)] for s, M in enumerate(sizes)]
+    batch, refs = assemble([lower_fleet(devs, llama_online_model, "4bit") for devs in fleets], [ks] * len(fleets))
+    for f in ("col_idx", "val", "col_lb", "row_lb", "row_ub"):
+        setattr(batch, f, getattr(batch, f).copy())
+
+    def inst(fleet, k):
+        return next(j for j, r in enumerate(refs) if r.fleet == fleet and r.k == k)
+
+    def eq_start(j):
+        m = int(batch.n_rows[j])
+        return int(batch.row_ptr[batch.csr_off[j] + m - 1])
+
+    batch.val[eq_start(inst(6, 1)) + 1] = 2.0                      # a coefficient 2 (every k of fleet 6)
+    e = eq_start(inst(7, 1))
+    batch.col_idx[e], batch.col_idx[e + 1] = batch.col_idx[e + 1], batch.col_idx[e]  # swapped columns
+    j = inst(8, 1)
+    batch.row_lb[batch.row_off[j] + batch.n_rows[j] - 1] -= 1.0    # row_lb != row_ub
+    j = inst(9, 1)
+    batch.row_lb[batch.row_off[j] + batch.n_rows[j] - 1] = batch.row_ub[batch.row_off[j] + batch.n_rows[j] - 1] = 79.5
+    batch.col_lb[batch.col_off[inst(10, 1)] + 3] = -1.0             # a negative w lower bound
+    batch.col_lb[batch.col_off[inst(11, 2)] + 15] = np.nan          # a NaN w lower bound (counts 0)
+    want = ctx.solve(batch)
+    settled = np.zeros(batch.n_inst, np.uint8) if flags == "none" else settled_instances(batch)
+    got = _device_solve(ctx, batch, settled, dev, torch.cuda.Stream(dev))
+    assert np.array_equal(got["status"], want.status), (got["status"], want.status)
+    for f in ("obj_lin", "dual_bound", "gap", "nodes"):
+        assert np.array_equal(got[f], getattr(want, f)), f
+    for i in np.flatnonzero(want.status == 0):
+        a, b = int(batch.col_off[i]), int(batch.col_off[i] + batch.n_cols[i])
+        assert np.array_equal(got["x"][a:b], want.x[a:b])
+    # every verdict kind occurred
+    assert {0, 2, -1} <= set(want.status.tolist())
