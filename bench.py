@@ -25,6 +25,7 @@ region between a barrier and its device's synchronize; the max over ranks is rep
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -112,8 +113,11 @@ def algorithmic_bytes(lowered, refs, n_k: int, settled=None):
     instance its status, per optimal instance its header, c and x, per fleet the offsets in and best k,
     obj_value and w / n out, obj_by_k / status when requested (not in the bench). `settled` (one flag per
     instance, halda_solve_batch_device_settled): a settled instance costs the screen its header, its flag,
-    its verdict byte and the result scalars."""
-    solve = screen = lower = pick = 0
+    its verdict byte and the result scalars. halda_solve_k1_settled_kernel (a settled batch: no screen
+    launch, the k = 1 kernel screens the unsettled instances on its way, whose screen reads are part of
+    the solve's): the solve's bytes plus per instance its flag and verdict byte, and a settled instance's
+    result scalars."""
+    solve = screen = lower = pick = fused = 0
     fleets_seen, fleets_solved = set(), set()
     for i, ref in enumerate(refs):
         fl = lowered[ref.fleet]
@@ -121,6 +125,7 @@ def algorithmic_bytes(lowered, refs, n_k: int, settled=None):
         csr = 4 * (nr + 1) + 12 * fl.nnz
         scr = HDR + 1 + 1 if settled is not None and settled[i] else HDR + 8 + 12 * M + 16 + 8 * M + 8 + 1
         screen += scr
+        fused += 2 + (RES if settled is not None and settled[i] else 0)
         if ref.fleet not in fleets_seen:
             fleets_seen.add(ref.fleet)
             lower += DEV_FIELDS * M + 8 + csr + 24
@@ -142,7 +147,7 @@ def algorithmic_bytes(lowered, refs, n_k: int, settled=None):
     # launch (register or lane-segment kernel), or the table kernel when it runs the whole batch alone
     # (as the dominant launch it does; as the gated second launch it only redoes flagged fleets)
     sweep = sum(DEV_FIELDS * fl.M + 8 + 4 + 8 + 8 * fl.M for fl in lowered)
-    return {"halda_screen_kernel": screen, "halda_solve_k1_kernel": solve,
+    return {"halda_screen_kernel": screen, "halda_solve_k1_kernel": solve, "halda_solve_k1_settled_kernel": solve + fused,
             "halda_lower_kernel": lower, "halda_pick_kernel": pick, "halda_sweep_kernel": sweep,
             "halda_sweep_seg_kernel": sweep, "halda_sweep_tables_kernel": sweep}
 
@@ -641,6 +646,21 @@ def c2_leg(args, torch, dev, ctx, model, stream, srefs):
     }
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 sent to fd 2 for the block (native libraries that print to stdout: RCCL's banner,
+    gloo's connection lines), so that the bench's stdout holds its JSON line alone."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
     """Latency mode (halda_p_solver.py:391-412 is the k loop it shards): the k-sweep of
     one C2 fleet and of 4096 C2 fleets through halda_solve_fleets_sharded over a real one-rank RCCL
@@ -655,7 +675,8 @@ def latency_leg(torch, dev, ctx, model, stream, runs: int = 50):
 
     out = {}
     try:
-        comm = RcclComm(1, 0, RcclComm.unique_id(), dev.index or 0)
+        with stdout_to_stderr():  # RCCL prints its version banner on stdout: keep stdout the one JSON line
+            comm = RcclComm(1, 0, RcclComm.unique_id(), dev.index or 0)
     except Exception as e:  # noqa: BLE001
         comm = None
         out["rccl_error"] = str(e)[:200]
@@ -837,10 +858,12 @@ def main():
     torch.cuda.set_device(local)  # before the process group: its barriers run on this rank's GPU
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", init_method="env://", device_id=dev)
-        else:
-            dist.init_process_group("gloo", init_method="env://")
+        with stdout_to_stderr():
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", init_method="env://", device_id=dev)
+            else:
+                dist.init_process_group("gloo", init_method="env://")
+            dist.barrier()  # the backends connect (and print) on first use
         rccl_world = dist.get_world_size()
         if rccl_world != args.gpus:
             print(f"bench.py: RCCL world size {rccl_world} != --gpus {args.gpus}", file=sys.stderr)

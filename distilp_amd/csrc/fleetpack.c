@@ -273,6 +273,17 @@ static void prefetch_tables(const Job *J, PyObject *d, int keys) {
 
 static void *worker(void *arg) {
     const Job *J = (const Job *)arg;
+    if (J->nd < 8192) {  /* a small table (one halda_solve): cache-resident, two shallow stages */
+        for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g) {
+            if (g + 3 < J->hi) {
+                PyObject *d = dev_dict(J->devs[g + 3]);
+                if (d) prefetch_values(d);
+            }
+            PyObject *d = dev_dict(J->devs[g]);
+            if (!d || !fdict(d) || fast_dev(J, d, g)) *J->bail = 1;
+        }
+        return NULL;
+    }
     for (Py_ssize_t g = J->lo; g < J->hi && !*J->bail; ++g) {
         if (g + PF_OBJ < J->hi) __builtin_prefetch(J->devs[g + PF_OBJ]);
         if (g + PF_DICT < J->hi) {

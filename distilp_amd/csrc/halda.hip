@@ -127,6 +127,7 @@ struct Ctx {
     bool x_zero = true;            // fused sweep: x / c of non-optimal instances written as zeros
     bool host_copy = false;        // halda_solve_fleets_host: PCIe copies even for small calls (HALDA_HOST_PATH=copy)
     bool fused_screen = true;      // a settled batch screens inside its k = 1 kernel (HALDA_FUSED_SCREEN=0: screen launch)
+    bool fused_last = false;       // the last CSR launch screened in its k = 1 kernel (halda_last_phase_ms)
     bool last_fleet_fused = false;
     int path_gen = 0;              // bumped by halda_set_fleets_path: prepared plans re-plan on their next launch
     void *shard = nullptr;         // rank-local results of halda_solve_fleets_sharded
@@ -366,7 +367,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
     if (settled && ctx->fused_screen) {
         // a settled batch: no screen launch -- the persistent k = 1 kernel writes the settled instances'
         // outputs and screens every other instance on its way (halda_solve_k1_settled_kernel)
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->evk, stream));
+        ctx->fused_last = true;
         int per_cu = 0;
         HIP_TRY(ctx->occupancy(reinterpret_cast<const void *>(halda_solve_k1_settled_kernel), lds1, &per_cu));
         const int grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->cus) * per_cu, in.n_inst)));
@@ -374,6 +375,7 @@ int launch(Ctx *ctx, const halda_batch &in, const halda_result &out, hipStream_t
                            mmax, hb_flag, launch_id, settled, gen_flag, in.max_R1, int(tab), int(tab_kc));
         HIP_TRY(hipGetLastError());
     } else {
+        ctx->fused_last = false;
         // screen kernel (8 instances per wave), then a persistent k = 1 kernel
         const int64_t screen_waves = (int64_t(in.n_inst) + kScreenPer - 1) / kScreenPer;
         hipLaunchKernelGGL(halda_screen_kernel, dim3(unsigned((screen_waves + 3) / 4)), dim3(256), 0, stream, in, out,
@@ -1258,8 +1260,12 @@ int halda_last_phase_ms(void *ctx, double *ms3) {
     if (!c->timed) return fail(HALDA_E_ARG, "no solve has been launched on this context");
     HIP_TRY(hipEventSynchronize(c->ev1));
     float a = 0.f, b = 0.f, d = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evk));
-    HIP_TRY(hipEventElapsedTime(&b, c->evk, c->evs));
+    if (c->fused_last) {  // no screen launch: the settled k = 1 kernel from the start
+        HIP_TRY(hipEventElapsedTime(&b, c->ev0, c->evs));
+    } else {
+        HIP_TRY(hipEventElapsedTime(&a, c->ev0, c->evk));
+        HIP_TRY(hipEventElapsedTime(&b, c->evk, c->evs));
+    }
     HIP_TRY(hipEventElapsedTime(&d, c->evs, c->ev1));
     ms3[0] = a;
     ms3[1] = b;

@@ -344,11 +344,14 @@ class HaldaContext:
         return {n: float(v) for n, v in zip(names, ms) if v > 0.0}
 
     def last_phase_ms(self) -> Dict[str, float]:
-        """Device time of each launch of the last solve: screen, k = 1 fast path, general kernel."""
+        """Device time of each launch of the last solve: screen, k = 1 fast path, general kernel. A settled
+        batch has no screen launch: its k = 1 kernel is halda_solve_k1_settled_kernel (include/halda.h)."""
         ms = (ctypes.c_double * 3)()
         rc = self.lib.halda_last_phase_ms(self.ctx, ms)
         if rc != 0:
             raise RuntimeError(f"halda_last_phase_ms failed ({rc}): {last_error(self.lib)}")
+        if ms[0] == 0.0:
+            return {"halda_solve_k1_settled_kernel": ms[1], "halda_solve_kernel": ms[2]}
         return {"halda_screen_kernel": ms[0], "halda_solve_k1_kernel": ms[1], "halda_solve_kernel": ms[2]}
 
 

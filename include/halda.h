@@ -123,7 +123,9 @@ int halda_solve_batch_device(void *ctx, const halda_batch *in, halda_result *out
  * over W = L/k < M layers: the k's milp() returns res.success == False,
  * halda_p_solver.py:369-436). Its result is written as HALDA_STATUS_INFEASIBLE
  * (the screen's own verdict for it: obj_lin = dual_bound = gap = inf, nodes 0)
- * and none of its rows or column bounds is read; only its header entries are.
+ * and nothing of it but its flag is read. The batch has no screen launch: its
+ * k = 1 kernel (halda_solve_k1_settled_kernel) writes the settled outputs and
+ * screens every other instance on the way, with the screen's rules.
  * settled[i] == 0 instances are solved as by halda_solve_batch_device, bit for
  * bit; settled == NULL is halda_solve_batch_device. A settled flag on an
  * instance that is not infeasible is the caller's error (it is not checked). */
@@ -142,7 +144,9 @@ int halda_set_timing(void *ctx, int on);
 
 /* Device time of the last solve per launch, in ms: ms3[0] the screen kernel
  * (halda_screen_kernel), ms3[1] the persistent k = 1 kernel (halda_solve_k1_kernel),
- * ms3[2] the general kernel's launches (k > 1, then k = 1 wide / hand-backs). */
+ * ms3[2] the general kernel's launches (k > 1, then k = 1 wide / hand-backs). A settled batch
+ * (halda_solve_batch_device_settled) has no screen launch: ms3[0] = 0 and ms3[1] is its k = 1 kernel
+ * (halda_solve_k1_settled_kernel, which screens on its way). */
 int halda_last_phase_ms(void *ctx, double *ms3);
 
 /* ------------------------------------------------------------------------
