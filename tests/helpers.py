@@ -51,3 +51,39 @@ def load_golden_lowered(z, key):
         "c": z[key + "_c"], "lb": z[key + "_lb"], "ub": z[key + "_ub"], "integrality": z[key + "_integrality"],
         "b_ub": z[key + "_bub"], "A_eq": z[key + "_Aeq"], "b_eq": z[key + "_beq"], "A_ub": A,
     }
+
+
+def replicate_batch(keep, batch, settled_dev, G: int, torch):
+    """G copies of a device-resident CSR batch as ONE batch (a caller with G batches of instances may hand
+    them to the milp() replacement as one): every array repeated, the offsets of copy g shifted past the
+    copies before it (row_ptr by g x nnz, csr_off by g x row_ptr entries, col_off / row_off by g x the
+    column / row totals). Returns (device arrays, result arrays, settled flags, shape record)."""
+    import types
+
+    nnz, nrp = int(keep["col_idx"].numel()), int(keep["row_ptr"].numel())
+    ncol, nrow = int(keep["c"].numel()), int(keep["row_lb"].numel())
+    if G * nnz >= 2 ** 31:
+        raise ValueError("replicated batch too large for int32 row pointers")
+
+    def rep(t, step=None):
+        if step is None:
+            return t.repeat(G)
+        g = torch.arange(G, device=t.device, dtype=torch.int64).repeat_interleave(t.numel())
+        return (t.to(torch.int64).repeat(G) + g * step).to(t.dtype)
+
+    big = {"n_cols": rep(keep["n_cols"]), "n_rows": rep(keep["n_rows"]), "csr_off": rep(keep["csr_off"], nrp),
+           "col_off": rep(keep["col_off"], ncol), "row_off": rep(keep["row_off"], nrow),
+           "row_ptr": rep(keep["row_ptr"], nnz)}
+    for f in ("col_idx", "val", "c", "col_lb", "col_ub", "row_lb", "row_ub", "integrality"):
+        big[f] = rep(keep[f])
+    n = G * batch.n_inst
+    dev = keep["c"].device
+    out = {"status": torch.empty(n, dtype=torch.int32, device=dev),
+           "x": torch.zeros(G * ncol, dtype=torch.float64, device=dev),
+           "obj_lin": torch.empty(n, dtype=torch.float64, device=dev),
+           "dual_bound": torch.empty(n, dtype=torch.float64, device=dev),
+           "gap": torch.empty(n, dtype=torch.float64, device=dev),
+           "nodes": torch.empty(n, dtype=torch.int64, device=dev)}
+    shape = types.SimpleNamespace(n_inst=n, max_cols=batch.max_cols, max_R1=batch.max_R1, max_tab=batch.max_tab,
+                                  max_tab_kc=batch.max_tab_kc, mip_rel_gap=batch.mip_rel_gap)
+    return big, out, settled_dev.repeat(G), shape

@@ -123,3 +123,42 @@ def test_fused_screen_equals_screen_launch_on_hostile_batches(llama_online_model
         assert np.array_equal(got["x"][a:b], want.x[a:b])
     # every verdict kind occurred
     assert {0, 2, -1} <= set(want.status.tolist())
+
+
+@pytest.mark.parametrize("M,nf,G", [(64, 37, 7), (16, 40, 5)])
+def test_replicated_settled_batch_equals_each_copy(llama_online_model, M, nf, G):
+    """G batches handed over as ONE settled batch (helpers.replicate_batch: every array repeated, the offsets
+    of copy g shifted past the copies before it), in which the settled k = 1 kernel's persistent waves take
+    many open instances each (measured as a throughput form and not kept in the bench). Every copy's status, obj_lin,
+    dual_bound, gap, nodes and x equal the synchronous solve of the one batch, bit for bit (C3 shape: k = 1
+    fast path; C2 shape: k > 1 instances through the general launch behind it)."""
+    import torch
+
+    from distilp_amd.common import DeviceProfile
+
+    from .helpers import replicate_batch
+
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ks = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(8100 + 7 * M + s, M)] for s in range(nf)]
+    batch, _ = assemble([lower_fleet(devs, llama_online_model, "4bit") for devs in fleets], [ks] * nf)
+    want = ctx.solve(batch)
+    keep = {f: torch.from_numpy(np.ascontiguousarray(getattr(batch, f))).to(dev) for f in FIELDS}
+    settled = torch.from_numpy(settled_instances(batch)).to(dev)
+    big, out, hint, shape = replicate_batch(keep, batch, settled, G, torch)
+    torch.cuda.synchronize(dev)
+    ctx.solve_device({f: t.data_ptr() for f, t in big.items()}, shape, {f: t.data_ptr() for f, t in out.items()},
+                     stream=torch.cuda.Stream(dev).cuda_stream, settled=hint.data_ptr())
+    torch.cuda.synchronize(dev)
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    n, nc = batch.n_inst, batch.total_cols
+    for g in range(G):
+        sl = slice(g * n, (g + 1) * n)
+        assert np.array_equal(got["status"][sl], want.status), g
+        for f in ("obj_lin", "dual_bound", "gap", "nodes"):
+            assert np.array_equal(got[f][sl], getattr(want, f)), (g, f)
+        xg = got["x"][g * nc:(g + 1) * nc]
+        for i in np.flatnonzero(want.status == 0):
+            a, b = int(batch.col_off[i]), int(batch.col_off[i] + batch.n_cols[i])
+            assert np.array_equal(xg[a:b], want.x[a:b]), (g, i)
