@@ -2307,6 +2307,27 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
     d.Kf[0] = d.Kf[1] = 0;
     d.r1w = d.r2w = d.rhs1 = d.rhs2 = 0.0;
 
+    // the screen's verdict: everything but the equality row's entries is in (round trip 1), so it is
+    // decided here, before round trip 2 is issued, as far as it goes -- in screen_group's precedence: UNSUPPORTED (equality row),
+    // INFEASIBLE (w lower bounds), TOO_LARGE (the launches' slices), CLS_GEN (c[C] > 0) -- and only a
+    // scalar code and the row's start are kept; the entries come with the first cycle half below
+    // (screen_group's round trip 3), when the capacity rows' registers are free
+    int pre = 0, eqb = 0;  // pre: 0 a k = 1 candidate, else the HALDA_STATUS_* / -100 - CLS_GEN verdict
+    if constexpr (kScreen) {
+        const bool eq_ext = eqe - eqs == M;
+        eqb = eq_ext ? eqs : 0;
+        const bool lb_inf = wave_or(act && (int(ceil(lbv[0])) > I.W || lbv[0] < 0.0)) != 0;
+        if (!(Wl == I.Wd) || !(I.Wd >= 0.0 && I.Wd < 1e6 && I.Wd == floor(I.Wd)) || !eq_ext) {
+            pre = HALDA_STATUS_UNSUPPORTED;
+        } else if (lb_inf || sumlo > I.W) {
+            pre = HALDA_STATUS_INFEASIBLE;
+        } else {
+            const int R1 = I.W - sumlo + 1;
+            const bool kc = I.kc > 0.0;
+            if (R1 > sc->r1max || int64_t(M) * odd_stride(R1) > (kc ? sc->tab_kc : sc->tab)) pre = HALDA_STATUS_TOO_LARGE;
+            else if (kc) pre = -100 - CLS_GEN;
+        }
+    }
     // ---- round trip 2: capacity entries (LDS-DMA, coalesced), cycle row pointers / bounds
     const int nc = cend - cbase;
     if (nc < 0 || nc > kStage) return 2;
@@ -2338,27 +2359,6 @@ __device__ int decode_k1(const halda_batch &B, const WaveCtx &w, unsigned char *
     }
     stage_wait();  // staged entries and zeroed counters visible
     HALDA_DSTAMP(2);
-    // the screen's verdict: everything but the equality row's entries is in (round trip 1), so it is
-    // decided here as far as it goes -- in screen_group's precedence: UNSUPPORTED (equality row),
-    // INFEASIBLE (w lower bounds), TOO_LARGE (the launches' slices), CLS_GEN (c[C] > 0) -- and only a
-    // scalar code and the row's start are kept; the entries come with the first cycle half below
-    // (screen_group's round trip 3), when the capacity rows' registers are free
-    int pre = 0, eqb = 0;  // pre: 0 a k = 1 candidate, else the HALDA_STATUS_* / -100 - CLS_GEN verdict
-    if constexpr (kScreen) {
-        const bool eq_ext = eqe - eqs == M;
-        eqb = eq_ext ? eqs : 0;
-        const bool lb_inf = wave_or(act && (int(ceil(lbv[0])) > I.W || lbv[0] < 0.0)) != 0;
-        if (!(Wl == I.Wd) || !(I.Wd >= 0.0 && I.Wd < 1e6 && I.Wd == floor(I.Wd)) || !eq_ext) {
-            pre = HALDA_STATUS_UNSUPPORTED;
-        } else if (lb_inf || sumlo > I.W) {
-            pre = HALDA_STATUS_INFEASIBLE;
-        } else {
-            const int R1 = I.W - sumlo + 1;
-            const bool kc = I.kc > 0.0;
-            if (R1 > sc->r1max || int64_t(M) * odd_stride(R1) > (kc ? sc->tab_kc : sc->tab)) pre = HALDA_STATUS_TOO_LARGE;
-            else if (kc) pre = -100 - CLS_GEN;
-        }
-    }
     auto screen_verdict = [&](int ecol, double eval) -> bool {
         sc->screened = true;
         int st = 0, v = CLS_K1;
@@ -2717,16 +2717,14 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_se
     unsigned char *sval = smem + sl.stage + kStageColBytes;
     K1Screen sc{mmax, r1max, tab, tab_kc, gen_flag, launch_id, cls, &Rz, false};
     const int S = gridDim.x;
-    {
-        // the screen's outputs for the settled instances (screen_group: hint) of a contiguous stretch per
-        // wave, lane = instance: coalesced stores (the strided walk below would scatter them one line each)
-        const int64_t per = (B.n_inst + S - 1) / S, end = min(B.n_inst, (int64_t(blockIdx.x) + 1) * per);
-        for (int64_t i = int64_t(blockIdx.x) * per + lane; i < end; i += 64)
-            if (settled[i]) {
-                cls[i] = CLS_DONE;
-                write_done(Rz, int(i), HALDA_STATUS_INFEASIBLE, 0);
-            }
-    }
+    // the screen's outputs for the settled instances (screen_group: hint), 64 consecutive instances per
+    // wave and pass, lane = instance: whole-line stores (the strided walk below would scatter them one
+    // line each; a stretch of n / gridDim instances per wave left partial lines: +5 MB of writes at C3)
+    for (int64_t i = int64_t(blockIdx.x) * 64 + lane; i - lane < B.n_inst; i += int64_t(64) * S)
+        if (i < B.n_inst && settled[i]) {
+            cls[i] = CLS_DONE;
+            write_done(Rz, int(i), HALDA_STATUS_INFEASIBLE, 0);
+        }
     for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
         const int64_t mine = base + int64_t(lane) * S;
         const bool in = mine < B.n_inst;
