@@ -240,3 +240,23 @@ def test_c_abi_objective_against_halda_solve(fixtures_golden, llama_online_model
             n_bits += got == want.obj_value
     assert n_cmp == 24 + 1024
     print(f"C ABI obj_value bit-equal to halda_solve's on {n_bits} of {n_cmp}")
+
+
+@pytest.mark.parametrize("want_x", ["open", True])
+def test_page_locked_workspaces_equal_staged_copies(llama_online_model, want_x):
+    """halda_solve_fleets_host with every array in halda_host_alloc blocks (the batch API's workspaces) DMAs
+    straight from and to them; with pageable arrays it stages through the context's own buffer. Both give
+    the same best k, obj_value, w, n, per-k objectives, statuses and x / c, bit for bit, on a batch above
+    the zero-copy size (300 C3 fleets) -- compact ("open") and dense x / c layouts."""
+    from distilp_amd.solver import fleets as FL
+
+    fleets = [[DeviceProfile.model_validate(d) for d in synth_fleet(9100 + s, 64)] for s in range(300)]
+    pageable = fleet_table(fleets, llama_online_model)
+    want = solve_table(pageable, llama_online_model, KS80, 0.5, want_x=want_x)
+    pinned = fleet_table(fleets, llama_online_model, _reuse=True)
+    assert FL._PINNED_OK, "halda_host_alloc failed on a GPU box"
+    got = solve_table(pinned, llama_online_model, KS80, 0.5, want_x=want_x, _reuse=True)
+    for f in ("best_k", "obj_value", "w", "n", "obj_by_k", "status", "x", "c"):
+        assert np.array_equal(getattr(got, f), getattr(want, f)), f
+    if want_x == "open":
+        assert np.array_equal(got.x_off, want.x_off)
