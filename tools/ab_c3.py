@@ -10,7 +10,7 @@ import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-KS = [1, 2, 4, 5, 8, 10, 16, 20, 40]
+KS = [int(k) for k in os.environ.get("HALDA_AB_KS", "1,2,4,5,8,10,16,20,40").split(",")]  # (diagnostic override)
 
 
 def main():
@@ -37,7 +37,7 @@ def main():
         dts[i % 16].launch(ctx, ss[0].cuda_stream)
     e1.record(ss[0])
     torch.cuda.synchronize(dev)
-    out = {"lib": os.environ.get("HALDA_LIB", "default"), "M": M, "one_launch_us": e0.elapsed_time(e1) / 200 * 1e3}
+    out = {"lib": os.environ.get("HALDA_LIB", "default"), "M": M, "ks": KS, "one_launch_us": e0.elapsed_time(e1) / 200 * 1e3}
     for steps in (200, 20, 200, 20):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
