@@ -2717,16 +2717,21 @@ __global__ __launch_bounds__(64, HALDA_K1_WAVES_PER_SIMD) void halda_solve_k1_se
     unsigned char *sval = smem + sl.stage + kStageColBytes;
     K1Screen sc{mmax, r1max, tab, tab_kc, gen_flag, launch_id, cls, &Rz, false};
     const int S = gridDim.x;
+    const int vb = blockIdx.x;  // (an XCD-grouped map, consecutive instances on one XCD: -2 % fetch, no faster)
     // the screen's outputs for the settled instances (screen_group: hint), 64 consecutive instances per
     // wave and pass, lane = instance: whole-line stores (the strided walk below would scatter them one
     // line each; a stretch of n / gridDim instances per wave left partial lines: +5 MB of writes at C3)
-    for (int64_t i = int64_t(blockIdx.x) * 64 + lane; i - lane < B.n_inst; i += int64_t(64) * S)
+    for (int64_t i = int64_t(vb) * 64 + lane; i - lane < B.n_inst; i += int64_t(64) * S)
         if (i < B.n_inst && settled[i]) {
             cls[i] = CLS_DONE;
             write_done(Rz, int(i), HALDA_STATUS_INFEASIBLE, 0);
         }
-    for (int64_t base = blockIdx.x; base < B.n_inst; base += int64_t(64) * S) {
-        const int64_t mine = base + int64_t(lane) * S;
+    for (int64_t base = vb; base < B.n_inst; base += int64_t(64) * S) {
+        // lane * S formed again on every pass (asm: not hoisted out of the loop): held across the
+        // instances it was the kernel's one spill, 512 B of scratch written and read per wave
+        int ls;
+        asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(ls) : "v"(lane), "s"(S));
+        const int64_t mine = base + ls;
         const bool in = mine < B.n_inst;
         const bool done = in && settled[in ? mine : 0] != 0;
         uint64_t todo = __ballot(in && !done);
