@@ -689,18 +689,51 @@ done:
  * sets=...) gives: the field dict, its own fields-set, no extra / private state. */
 static PyObject *s_dict, *s_fset, *s_extra, *s_priv, *s_w, *s_n, *s_k, *s_obj, *s_sets, *s_m[3], *s_fields_tpl;
 
+/* The interpreter's small ints 0 .. kSmall - 1 (layer counts, device indices), fetched once per results()
+ * call: each entry of a list is then one load and an incref, not a PyLong_From* call per entry (that call
+ * finds the interpreter state every time; 2 x 64 + 64 entries per fleet). Borrowed: the interpreter keeps
+ * its small ints alive. */
+enum { kSmall = 257 };
+static PyObject *g_small[kSmall];
+
+static int small_ints(void) {
+    if (g_small[0]) return 0;
+    for (int i = 0; i < kSmall; ++i) {
+        PyObject *o = PyLong_FromLong(i);
+        if (!o) return -1;
+        g_small[i] = o; /* a cached small int: the reference held here is never dropped */
+    }
+    return 0;
+}
+
+static PyObject *int_of(double v) {
+    /* int(round(v)), half to even; an integral v (every w / n the solve writes) skips the rounding */
+    const double r = fabs(v) < 9.0e18 && v == (double)(long long)v ? v : nearbyint(v);
+    if (r >= 0.0 && r < (double)kSmall) {
+        PyObject *o = g_small[(int)r];
+        Py_INCREF(o);
+        return o;
+    }
+    return fabs(r) < 9.0e18 ? PyLong_FromLongLong((long long)r) : PyLong_FromDouble(r);
+}
+
 static PyObject *int_list(const double *v, Py_ssize_t M) {
     PyObject *l = PyList_New(M);
     if (!l) return NULL;
     for (Py_ssize_t i = 0; i < M; ++i) {
-        /* the int of the rounded double (int(round(x)), half to even); a layer count is a small int,
-         * which PyLong_FromLong takes from the interpreter's cache, no allocation */
-        const double r = nearbyint(v[i]);
-        PyObject *o = fabs(r) < 9.0e18 ? PyLong_FromLongLong((long long)r) : PyLong_FromDouble(r);
+        PyObject *o = int_of(v[i]);
         if (!o) { Py_DECREF(l); return NULL; }
         PyList_SET_ITEM(l, i, o);
     }
     return l;
+}
+
+static PyObject *index_of(Py_ssize_t i) {
+    if (i < kSmall) {
+        Py_INCREF(g_small[i]);
+        return g_small[i];
+    }
+    return PyLong_FromSsize_t(i);
 }
 
 /* Where model_construct's four stores land in an instance of `cls`: the instance dict's offset and the
@@ -765,7 +798,7 @@ static PyObject *one_result(PyTypeObject *cls, PyObject *noargs, const double *x
         if (!(v = PyList_New(cnt))) goto fail;
         for (Py_ssize_t i = 0, j = 0; i < M; ++i)
             if (cls_row[i] == s) {
-                PyObject *ix = PyLong_FromSsize_t(i);
+                PyObject *ix = index_of(i);
                 if (!ix) goto fail;
                 PyList_SET_ITEM(v, j++, ix);
             }
@@ -816,7 +849,7 @@ static PyObject *sets_of(PyObject *self, PyObject *args) {
         if (!(v = PyList_New(cnt))) goto fail;
         for (Py_ssize_t i = 0, j = 0; i < M; ++i)
             if (cl[i] == s) {
-                PyObject *ix = PyLong_FromSsize_t(i);
+                PyObject *ix = index_of(i);
                 if (!ix) goto fail;
                 PyList_SET_ITEM(v, j++, ix);
             }
@@ -905,5 +938,6 @@ PyMODINIT_FUNC PyInit__fleetpack(void) {
         Py_DECREF(names);
         if (!s_fields_tpl) return NULL;
     }
+    if (small_ints()) return NULL;
     return PyModule_Create(&mod);
 }

@@ -324,6 +324,9 @@ def test_batch_results_c_builder_equals_python(llama_online_model, monkeypatch, 
     st = np.where(xo.reshape(nf, nk) >= 0, 0, 2).astype(np.int32)
     st[3 % nf, :] = 2  # a fleet without a feasible k
     x = rng.integers(0, 9, 2 * ext).astype(np.float64) + np.where(rng.random(2 * ext) < 0.3, 0.5, 0.0)
+    # values beyond the builder's small-int table and below 0, integral and half-way
+    odd = np.array([255.5, 256.0, 256.5, 257.0, 300.5, 1e6, -0.5, -2.5, -3.0, 2.0 ** 40 + 0.5])
+    x[:ext] = np.where(rng.random(ext) < 0.05, rng.choice(odd, ext), x[:ext])
     x[ext:] = rng.normal(size=ext)
     res = FleetSolve(best_k=None, obj_value=None, w=None, n=None, obj_by_k=None, status=st, ks=ks, x=x[:ext],
                      c=x[ext:], x_off=xo)
