@@ -56,7 +56,8 @@ def _full(world=1):
         "strong": {"fleets_total": 4096, "ms_per_step": _f(52), "instances_per_s": _f(53)} if world > 1 else None,
         "latency_mode": lat if world == 1 else None,
         "setup_s": _f(54), "fleets_per_s": _f(55),
-        "c5_stream": {"ms_per_batch": _f(56), "fleets_per_s": _f(57), "instances_per_s": _f(58)} if world == 1 else None,
+        "c5_stream": {"ms_per_batch": _f(56), "fleets_per_s": _f(57), "instances_per_s": _f(58),
+                      "reprofile_ms": _f(59)} if world == 1 else None,
         "solve_only": {"instances_per_s": _f(60), "ms_per_step": _f(61), "ms_per_step_one_stream": _f(62),
                        "ms_per_step_no_settled": _f(63), "ms_per_step_one_stream_no_settled": _f(64),
                        "settled_per_step": 32768, "streams": 2, "resident_copies": 2, "roofline": dict(roof)},
@@ -93,6 +94,7 @@ def test_compact_line_fits_and_ends_with_the_metric_figures():
     assert list(one["c2"])[-1] == "ms_per_step" and list(one["solve_only"])[-1] == "ms_per_step"
     assert one["roofline"]["valu_issue"]["fp64_per_item"] is not None
     assert one["time_to_optimal_parts"]["pack_ms"] is not None
+    assert list(one["c5_stream"])[-1] == "ms_per_batch" and one["c5_stream"]["reprofile_ms"] is not None
     eight = bench.compact_line(_full(8))
     assert eight["weak_200"]["ms_per_step"] is not None and eight["config"]["rccl_world_size"] == 8
 
