@@ -104,3 +104,42 @@ def test_plan_entry_points_reject_bad_arguments(lib):
     assert raw.halda_fleets_plan_launch(None, None) == -22
     raw.halda_set_fleets_path.argtypes = [P, ctypes.c_int]
     assert raw.halda_set_fleets_path(None, 1) == -22
+
+
+LLVM = __import__("pathlib").Path("/opt/rocm/lib/llvm/bin")
+
+
+def kernel_resources(tmp_path):
+    """Per kernel of libhalda's gfx950 code object: the AMDGPU metadata the compiler wrote (scratch bytes
+    per lane, VGPRs, spills), read from the .hip_fatbin bundle with the ROCm LLVM tools."""
+    import subprocess
+
+    tools = [LLVM / t for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf")]
+    if not all(t.exists() for t in tools):
+        pytest.skip("ROCm LLVM tools not found")
+    fat, co = tmp_path / "fatbin.bin", tmp_path / "gfx950.co"
+    subprocess.run([str(tools[0]), f"--dump-section=.hip_fatbin={fat}", str(lh.LIB_PATH), str(tmp_path / "host.so")],
+                   check=True, capture_output=True)
+    subprocess.run([str(tools[1]), "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+    notes = subprocess.run([str(tools[2]), "--notes", str(co)], check=True, capture_output=True, text=True).stdout
+    out = {}
+    for item in re.split(r"(?m)^  - \.agpr_count:", notes)[1:]:
+        kv = dict(re.findall(r"(?m)^    \.(\w+):\s+(\S+)", item))
+        out[re.search(r"halda_\w+?_kernel", kv["name"]).group(0)] = {
+            k: int(kv[k]) for k in ("private_segment_fixed_size", "vgpr_count", "vgpr_spill_count")}
+    return out
+
+
+def test_hot_kernels_use_no_scratch_at_their_occupancy(lib, tmp_path):
+    """The kernels the bench times keep every value in registers (no scratch) within the VGPR budget of
+    the occupancy DESIGN.md states: the C3 group launch at seven waves per SIMD (<= 72), the C2 k-slot
+    group launch at five four-wave workgroups per CU (<= 96), path B's k = 1 kernels at four (<= 128)."""
+    res = kernel_resources(tmp_path)
+    budget = {"halda_sweep_steps_kernel": 72, "halda_sweep_kslot_steps_kernel": 96,
+              "halda_solve_k1_settled_kernel": 128, "halda_solve_k1_kernel": 128, "halda_sweep_kernel": 128,
+              "halda_screen_kernel": 128, "halda_resident_kernel": 128}
+    for name, vgprs in budget.items():
+        r = res[name]
+        assert r["private_segment_fixed_size"] == 0 and r["vgpr_spill_count"] == 0, (name, r)
+        assert r["vgpr_count"] <= vgprs, (name, r)
