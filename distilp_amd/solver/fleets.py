@@ -124,12 +124,33 @@ def _bind(lib):
     return lib
 
 
+_MODEL_STRUCTS: dict = {}
+_ABSENT = object()
+
+
 def model_struct(model: ModelProfile, kv_factor: float) -> HaldaModelC:
+    """The C ABI's halda_model of `model` at `kv_factor` (read-only for every caller). Remembered by the
+    values it is made from -- every field it reads -- so a repeated halda_solve reuses it (a model
+    edited between calls gives another key)."""
     fq, fo = model.f_q, model.f_out
     has_q, has_o = "b_1" in fq, "b_1" in fo
-    return HaldaModelC(float(fq["b_1"]) if has_q else 0.0, float(fo["b_1"]) if has_o else 0.0, int(has_q),
-                       int(has_o), float(b_prime(model, kv_bits_k=kv_factor)), float(model.b_layer),
-                       float(model.b_in), float(model.b_out), float(model.V), int(model.L))
+    key = (fq.get("b_1", _ABSENT), fo.get("b_1", _ABSENT), kv_factor, model.hk, model.ek, model.hv, model.ev,
+           model.n_kv, model.b_layer, model.b_in, model.b_out, model.V, model.L)
+    try:
+        # (a zero anywhere: made afresh -- 0.0 and -0.0 are one dict key but not one struct)
+        hit = None if 0.0 in key else _MODEL_STRUCTS.get(key)
+    except TypeError:  # an unhashable field value: made afresh
+        key, hit = None, None
+    if hit is not None:
+        return hit
+    m = HaldaModelC(float(fq["b_1"]) if has_q else 0.0, float(fo["b_1"]) if has_o else 0.0, int(has_q),
+                    int(has_o), float(b_prime(model, kv_bits_k=kv_factor)), float(model.b_layer),
+                    float(model.b_in), float(model.b_out), float(model.V), int(model.L))
+    if key is not None and 0.0 not in key:
+        if len(_MODEL_STRUCTS) >= 64:
+            _MODEL_STRUCTS.clear()
+        _MODEL_STRUCTS[key] = m
+    return m
 
 
 @dataclass

@@ -101,6 +101,7 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
     st_list: List[int] = []
     xrow: List[int] = []
     out: List[Tuple[int, Optional[ILPResult]]] = []
+    j = -1  # k's index in pos (Ks ascending and distinct)
     for k in Ks:
         if debug:
             print("k: " + str(k))
@@ -110,12 +111,13 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
             raise err
         r: Optional[ILPResult] = None
         if k > 0:
+            j += 1
             if not swept:
                 swept = True
                 if one:
                     sweep_one(ws, model, kv_factor, device)
                     status, X, C, xrow = ws.status, ws.x, ws.c, ws.xrow
-                    t_comm, xi_sum, kappa = (float(v) for v in ws.consts)
+                    t_comm, xi_sum, kappa = ws.consts.tolist()
                     cls_row = ws.u8[0]
                 else:
                     res = solve_table(ws, model, pos, kv_factor, device, want_x=True)
@@ -127,7 +129,6 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                 if _cls_out is not None:
                     _cls_out.append(np.array(cls_row, np.uint8))
                 st_list = status.tolist()
-            j = pos.index(k)
             st = st_list[j]
             if st == STATUS_OPTIMAL:
                 # views of the rows (the workspace is read before this thread's next call): c.dot(x) is
