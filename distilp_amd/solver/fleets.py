@@ -632,6 +632,8 @@ class _OneFleet:
         self.c = self.fbuf[o2 + no * xs:].reshape(no, xs)
         self.res = HaldaFleetResultC(pI, pF, pI + 4, pI + 4 * (1 + nd), pF + 8, pI + 4 * (1 + 2 * nd), pF + 8 * o2,
                                      pF + 8 * (o2 + no * xs), self.x_off.ctypes.data)
+        # the call's arguments made once (ndarray.ctypes and byref cost microseconds per call)
+        self.karr_p, self.fs_ref, self.res_ref = self.karr.ctypes.data, ctypes.byref(self.fs), ctypes.byref(self.res)
 
 
 
@@ -660,8 +662,7 @@ def sweep_one(ws: "_OneFleet", model: ModelProfile, kv_factor: float, device: in
     lib = _bind(ctx.lib)
     m = model_struct(model, kv_factor)
     with ctx._lock:
-        rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ctypes.byref(ws.fs), ws.karr.ctypes.data,
-                                         len(ws.ks), ctypes.byref(ws.res))
+        rc = lib.halda_solve_fleets_host(ctx.ctx, ctypes.byref(m), ws.fs_ref, ws.karr_p, len(ws.ks), ws.res_ref)
     if rc != 0:
         raise RuntimeError(f"halda_solve_fleets_host failed ({rc}): {last_error(lib)}")
     fo = model.f_out

@@ -127,7 +127,7 @@ def _sweep_on_gpu(devs, model: ModelProfile, sets, Ks: List[int], kv_factor: flo
                     t_comm, xi_sum, kappa = (float(v[0]) for v in fleet_constants(ws, model))
                     cls_row = ws.os_class
                 if _cls_out is not None:
-                    _cls_out.append(np.array(cls_row, np.uint8))
+                    _cls_out.append(cls_row.tobytes())
                 st_list = status.tolist()
             st = st_list[j]
             if st == STATUS_OPTIMAL:
